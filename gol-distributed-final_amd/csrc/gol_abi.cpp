@@ -1,0 +1,541 @@
+// gol_abi.cpp -- C ABI of libgolhip.so: library entry points, the single-GPU
+// engine and the device launchers (include/golhip.h).
+//
+// The engine keeps the board resident in HBM and replaces the reference's
+// per-turn state handling in broker.go:62-234 (scatter of the whole board to
+// every worker, gather of the slabs, mirror copy into cWorld) with k-turn
+// kernel launches on a double-buffered bit board.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "golhip.h"
+#include "gol_internal.h"
+#include "gol_kernels.h"
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+int gol_set_error(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return gol_set_error(GOL_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                 __FILE__, __LINE__);                                             \
+    } while (0)
+
+extern "C" int gol_abi_version(void) { return GOL_ABI_VERSION; }
+extern "C" const char *gol_last_error(void) { return g_err.c_str(); }
+
+extern "C" int gol_device_count(int *n)
+{
+    if (!n) return gol_set_error(GOL_EINVAL, "n is NULL");
+    int c = 0;
+    HIPCHK(hipGetDeviceCount(&c));
+    *n = c;
+    return GOL_OK;
+}
+
+extern "C" int gol_partition_rows(int64_t H, int64_t parts, int64_t i, int64_t *y0, int64_t *y1)
+{
+    if (!y0 || !y1 || parts <= 0 || i < 0 || i >= parts || H < 0)
+        return gol_set_error(GOL_EINVAL, "bad partition arguments H=%lld parts=%lld i=%lld", (long long)H,
+                             (long long)parts, (long long)i);
+    // broker.go:135-139 (even) and broker.go:172-206 (first H%T slabs get one extra row)
+    const int64_t base = H / parts, rem = H % parts;
+    *y0 = i * base + std::min(i, rem);
+    *y1 = *y0 + base + (i < rem ? 1 : 0);
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------ worker path
+extern "C" int gol_next_state_slab(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0,
+                                   int64_t y1, uint8_t *out, int64_t out_stride)
+{
+    if (!world || !out || H <= 0 || W <= 0 || stride < W || out_stride < W || y0 < 0 || y1 > H || y0 > y1)
+        return gol_set_error(GOL_EINVAL, "bad slab arguments H=%lld W=%lld y0=%lld y1=%lld", (long long)H,
+                             (long long)W, (long long)y0, (long long)y1);
+    if (y0 == y1) return GOL_OK;
+    const int64_t ds = (W + 15) / 16 * 16;
+    uint8_t *dworld = nullptr, *dout = nullptr;
+    hipStream_t s = nullptr;
+    int rc = GOL_OK;
+    auto fail = [&](hipError_t e, const char *what) {
+        rc = gol_set_error(GOL_EHIP, "%s: %s", what, hipGetErrorString(e));
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) { fail(e, "stream"); return rc; }
+    if ((e = hipMalloc(&dworld, H * ds)) != hipSuccess) fail(e, "hipMalloc world");
+    else if ((e = hipMalloc(&dout, (y1 - y0) * ds)) != hipSuccess) fail(e, "hipMalloc slab");
+    else if ((e = hipMemcpy2DAsync(dworld, ds, world, stride, W, H, hipMemcpyHostToDevice, s)) != hipSuccess)
+        fail(e, "copy in");
+    else if ((e = golk_bytes_step(dworld, H, W, ds, y0, y1, dout, ds, s)) != hipSuccess) fail(e, "launch");
+    else if ((e = hipMemcpy2DAsync(out, out_stride, dout, ds, W, y1 - y0, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        fail(e, "copy out");
+    else if ((e = hipStreamSynchronize(s)) != hipSuccess) fail(e, "sync");
+    if (dworld) (void)hipFree(dworld);
+    if (dout) (void)hipFree(dout);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+// ------------------------------------------------------------------ engine
+static int pick_k(int want, int64_t remaining, int64_t H, int dw)
+{
+    static const int ks[] = {16, 8, 4, 2, 1};
+    for (int k : ks) {
+        if (k == 16 && dw > 2) continue;
+        if (k <= want && k <= remaining && k <= H) return k;
+    }
+    return 1;
+}
+
+static int engine_dev(gol_engine *e)
+{
+    HIPCHK(hipSetDevice(e->device));
+    return GOL_OK;
+}
+
+static void free_bytes(gol_engine *e)
+{
+    for (auto &b : e->bytes)
+        if (b) { (void)hipFree(b); b = nullptr; }
+}
+
+static int alloc_bytes(gol_engine *e)
+{
+    for (auto &b : e->bytes)
+        if (!b) HIPCHK(hipMalloc(&b, e->H * e->bstride));
+    return GOL_OK;
+}
+
+static int ensure_staging(gol_engine *e)
+{
+    if (!e->staging) {
+        // byte staging for chunked load/store/PGM: >= 1 row, <= 64 MiB
+        e->stage_rows = std::max<int64_t>(1, std::min<int64_t>(e->H, (64LL << 20) / e->bstride));
+        HIPCHK(hipMalloc(&e->staging, e->stage_rows * e->bstride));
+        HIPCHK(hipHostMalloc((void **)&e->host_staging, e->stage_rows * e->bstride, hipHostMallocDefault));
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, gol_engine **out)
+{
+    if (!out || H <= 0 || W <= 0 || W > (int64_t)INT32_MAX * 32 || H > INT32_MAX)
+        return gol_set_error(GOL_EINVAL, "bad board size %lldx%lld", (long long)W, (long long)H);
+    *out = nullptr;
+    gol_engine *e = new gol_engine();
+    e->H = H;
+    e->W = W;
+    e->bit_capable = (W % 64) == 0;
+    e->Wd = W / 32;
+    e->pitch = (e->Wd + 3) / 4 * 4;
+    e->bstride = (W + 15) / 16 * 16;
+    int dev = cfg ? cfg->device : -1;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    e->device = dev;
+    e->k = (cfg && cfg->turns_per_launch > 0) ? cfg->turns_per_launch : GOL_DEFAULT_K;
+    int cpl = (cfg && cfg->cells_per_lane > 0) ? cfg->cells_per_lane : 32 * GOL_DEFAULT_DW;
+    if (cpl != 32 && cpl != 64 && cpl != 128) {
+        delete e;
+        return gol_set_error(GOL_EINVAL, "cells_per_lane must be 32, 64 or 128");
+    }
+    e->dw = cpl / 32;
+    while (e->dw > 1 && (e->Wd % e->dw) != 0) e->dw >>= 1;
+    e->strip = cfg ? cfg->strip_rows : 0;
+    int rc = engine_dev(e);
+    if (rc == GOL_OK) {
+        hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+        if (he == hipSuccess) he = hipMalloc(&e->slots, GOL_COUNT_SLOTS * 8 * sizeof(uint64_t));
+        if (he == hipSuccess) he = hipMalloc(&e->flag, sizeof(uint32_t));
+        if (he == hipSuccess && e->bit_capable) {
+            for (auto &b : e->bits) {
+                he = hipMalloc(&b, H * e->pitch * sizeof(uint32_t));
+                if (he != hipSuccess) break;
+                he = hipMemset(b, 0, H * e->pitch * sizeof(uint32_t));
+                if (he != hipSuccess) break;
+            }
+            e->bit_mode = true;
+        }
+        if (he == hipSuccess && !e->bit_capable) {
+            rc = alloc_bytes(e);
+            if (rc == GOL_OK) he = hipMemset(e->bytes[0], 0, H * e->bstride);
+            e->bit_mode = false;
+        }
+        if (he != hipSuccess)
+            rc = gol_set_error(he == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP, "engine allocation: %s",
+                               hipGetErrorString(he));
+    }
+    if (rc != GOL_OK) {
+        gol_engine_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+extern "C" void gol_engine_destroy(gol_engine *e)
+{
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    for (auto &b : e->bits)
+        if (b) (void)hipFree(b);
+    free_bytes(e);
+    if (e->slots) (void)hipFree(e->slots);
+    if (e->flag) (void)hipFree(e->flag);
+    if (e->staging) (void)hipFree(e->staging);
+    if (e->host_staging) (void)hipHostFree(e->host_staging);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_t stride)
+{
+    if (!e || !world || stride < e->W) return gol_set_error(GOL_EINVAL, "bad load arguments");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    e->turn = 0;
+    if (!e->bit_capable) {
+        HIPCHK(hipMemcpy2DAsync(e->bytes[0], e->bstride, world, stride, e->W, e->H, hipMemcpyHostToDevice,
+                                e->stream));
+        e->bcur = 0;
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return GOL_OK;
+    }
+    // pack row chunks into the bit board; remember whether any byte is neither 0 nor 255
+    if ((rc = ensure_staging(e))) return rc;
+    HIPCHK(hipMemsetAsync(e->flag, 0, sizeof(uint32_t), e->stream));
+    e->cur = 0;
+    for (int64_t y = 0; y < e->H; y += e->stage_rows) {
+        const int64_t n = std::min(e->stage_rows, e->H - y);
+        HIPCHK(hipMemcpy2DAsync(e->staging, e->bstride, world + y * stride, stride, e->W, n,
+                                hipMemcpyHostToDevice, e->stream));
+        HIPCHK(golk_pack(e->staging, n, e->W, e->bstride, e->bits[0] + y * e->pitch, e->pitch, e->flag, e->stream));
+    }
+    uint32_t nonbinary = 0;
+    HIPCHK(hipMemcpyAsync(&nonbinary, e->flag, sizeof nonbinary, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (nonbinary) {
+        // exact first turn needs the bytes (worker.go:26-37): keep a byte board until turn 1
+        if ((rc = alloc_bytes(e))) return rc;
+        HIPCHK(hipMemcpy2DAsync(e->bytes[0], e->bstride, world, stride, e->W, e->H, hipMemcpyHostToDevice,
+                                e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->bcur = 0;
+        e->bit_mode = false;
+    } else {
+        free_bytes(e);
+        e->bit_mode = true;
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "random boards need W %% 64 == 0");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    free_bytes(e);
+    e->bit_mode = true;
+    e->cur = 0;
+    e->turn = 0;
+    HIPCHK(golk_random_fill(e->bits[0], e->H, 0, e->W, e->pitch, seed, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GOL_OK;
+}
+
+int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots)
+{
+    while (turns > 0) {
+        if (!e->bit_mode) {
+            const int nb = 1 - e->bcur;
+            HIPCHK(golk_bytes_step(e->bytes[e->bcur], e->H, e->W, e->bstride, 0, e->H, e->bytes[nb], e->bstride,
+                                   e->stream));
+            e->bcur = nb;
+            e->turn += 1;
+            turns -= 1;
+            if (e->bit_capable) {
+                // board is now strictly 0/255: continue on the bit board
+                HIPCHK(golk_pack(e->bytes[e->bcur], e->H, e->W, e->bstride, e->bits[0], e->pitch, nullptr,
+                                 e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                free_bytes(e);
+                e->cur = 0;
+                e->bit_mode = true;
+            }
+            continue;
+        }
+        const int k = pick_k(e->k, turns, e->H, e->dw);
+        const uint32_t *mid = e->bits[e->cur];
+        uint32_t *dst = e->bits[1 - e->cur];
+        const bool last = turns == k;
+        HIPCHK(golk_bits_step(mid + (e->H - k) * e->pitch, mid, mid, dst, e->H, e->Wd, e->pitch, 0, e->H, k, e->dw,
+                              e->strip, last ? count_slots : nullptr, e->stream));
+        e->cur = 1 - e->cur;
+        e->turn += k;
+        turns -= k;
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_step(gol_engine *e, int64_t turns)
+{
+    if (!e || turns < 0) return gol_set_error(GOL_EINVAL, "bad step arguments");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    if ((rc = gol_engine_step_async(e, turns, nullptr))) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_turn(gol_engine *e, int64_t *turn)
+{
+    if (!e || !turn) return gol_set_error(GOL_EINVAL, "bad arguments");
+    *turn = e->turn;
+    return GOL_OK;
+}
+
+static int sum_slots(gol_engine *e, uint64_t *out)
+{
+    std::vector<uint64_t> h(GOL_COUNT_SLOTS * 8);
+    HIPCHK(hipMemcpyAsync(h.data(), e->slots, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint64_t s = 0;
+    for (int i = 0; i < GOL_COUNT_SLOTS; ++i) s += h[i * 8];
+    *out = s;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_alive_count(gol_engine *e, uint64_t *count)
+{
+    if (!e || !count) return gol_set_error(GOL_EINVAL, "bad arguments");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(e->slots, 0, GOL_COUNT_SLOTS * 8 * sizeof(uint64_t), e->stream));
+    if (e->bit_mode)
+        HIPCHK(golk_popcount(e->bits[e->cur], e->H, e->Wd, e->pitch, e->slots, e->stream));
+    else
+        HIPCHK(golk_count_bytes(e->bytes[e->bcur], e->H, e->W, e->bstride, e->slots, e->stream));
+    return sum_slots(e, count);
+}
+
+extern "C" int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t stride)
+{
+    if (!e || !out || stride < e->W) return gol_set_error(GOL_EINVAL, "bad store arguments");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    if (!e->bit_mode) {
+        HIPCHK(hipMemcpy2DAsync(out, stride, e->bytes[e->bcur], e->bstride, e->W, e->H, hipMemcpyDeviceToHost,
+                                e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return GOL_OK;
+    }
+    if ((rc = ensure_staging(e))) return rc;
+    for (int64_t y = 0; y < e->H; y += e->stage_rows) {
+        const int64_t n = std::min(e->stage_rows, e->H - y);
+        HIPCHK(golk_unpack(e->bits[e->cur] + y * e->pitch, n, e->W, e->pitch, e->staging, e->bstride, e->stream));
+        HIPCHK(hipMemcpy2DAsync(out + y * stride, stride, e->staging, e->bstride, e->W, n, hipMemcpyDeviceToHost,
+                                e->stream));
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
+{
+    if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    const bool bm = e->bit_mode;
+    const void *board = bm ? (const void *)e->bits[e->cur] : (const void *)e->bytes[e->bcur];
+    const int64_t units = bm ? e->Wd : e->W, pitch = bm ? e->pitch : e->bstride;
+    int64_t *dcounts = nullptr;
+    int32_t *dxy = nullptr;
+    std::vector<int64_t> counts(e->H);
+    HIPCHK(hipMalloc(&dcounts, e->H * sizeof(int64_t)));
+    hipError_t he = golk_row_counts(bm, board, e->H, units, pitch, dcounts, e->stream);
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(counts.data(), dcounts, e->H * sizeof(int64_t), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    int64_t total = 0;
+    if (he == hipSuccess) {
+        for (auto &c : counts) {  // exclusive prefix -> first index of each row
+            const int64_t v = c;
+            c = total;
+            total += v;
+        }
+        *n = total;
+    }
+    const int64_t m = std::min(total, cap);
+    if (he == hipSuccess && m > 0) {
+        he = hipMemcpyAsync(dcounts, counts.data(), e->H * sizeof(int64_t), hipMemcpyHostToDevice, e->stream);
+        if (he == hipSuccess) he = hipMalloc(&dxy, m * 2 * sizeof(int32_t));
+        if (he == hipSuccess) he = golk_alive_list(bm, board, e->H, units, pitch, dcounts, dxy, m, e->stream);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(xy, dxy, m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    }
+    (void)hipFree(dcounts);
+    if (dxy) (void)hipFree(dxy);
+    if (he != hipSuccess) return gol_set_error(GOL_EHIP, "alive_cells: %s", hipGetErrorString(he));
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
+{
+    if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    if ((rc = ensure_staging(e))) return rc;
+    FILE *f = fopen(path, "wb");
+    if (!f) return gol_set_error(GOL_EIO, "cannot create %s", path);
+    // gol/io.go:52-59 header
+    fprintf(f, "P5\n%lld %lld\n255\n", (long long)e->W, (long long)e->H);
+    for (int64_t y = 0; y < e->H && rc == GOL_OK; y += e->stage_rows) {
+        const int64_t n = std::min(e->stage_rows, e->H - y);
+        hipError_t he;
+        if (e->bit_mode) {
+            he = golk_unpack(e->bits[e->cur] + y * e->pitch, n, e->W, e->pitch, e->staging, e->bstride, e->stream);
+            if (he == hipSuccess)
+                he = hipMemcpy2DAsync(e->host_staging, e->W, e->staging, e->bstride, e->W, n, hipMemcpyDeviceToHost,
+                                      e->stream);
+        } else {
+            he = hipMemcpy2DAsync(e->host_staging, e->W, e->bytes[e->bcur] + y * e->bstride, e->bstride, e->W, n,
+                                  hipMemcpyDeviceToHost, e->stream);
+        }
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) rc = gol_set_error(GOL_EHIP, "write_pgm: %s", hipGetErrorString(he));
+        else if (fwrite(e->host_staging, 1, (size_t)(n * e->W), f) != (size_t)(n * e->W))
+            rc = gol_set_error(GOL_EIO, "short write to %s", path);
+    }
+    if (fclose(f) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
+    return rc;
+}
+
+extern "C" int gol_engine_hash(gol_engine *e, uint64_t *hash)
+{
+    if (!e || !hash) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "hash needs W %% 64 == 0");
+    int rc = engine_dev(e);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(e->slots, 0, GOL_COUNT_SLOTS * 8 * sizeof(uint64_t), e->stream));
+    const uint32_t *bits = e->bits[e->cur];
+    if (!e->bit_mode) {  // loaded non-binary bytes at turn 0: hash the 255-cells
+        HIPCHK(golk_pack(e->bytes[e->bcur], e->H, e->W, e->bstride, e->bits[1 - e->cur], e->pitch, nullptr,
+                         e->stream));
+        bits = e->bits[1 - e->cur];
+    }
+    HIPCHK(golk_hash(bits, e->H, 0, e->Wd, e->pitch, e->slots, e->stream));
+    return sum_slots(e, hash);
+}
+
+extern "C" int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lane, int32_t *strip_rows,
+                               int32_t *bit_mode)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    if (k) *k = e->k;
+    if (cells_per_lane) *cells_per_lane = 32 * e->dw;
+    if (strip_rows) {
+        const int64_t ng = (e->Wd + 62 * e->dw - 1) / (62 * e->dw);
+        *strip_rows = e->strip > 0 ? e->strip : golk_auto_strip(e->H, ng, pick_k(e->k, e->k, e->H, e->dw));
+    }
+    if (bit_mode) *bit_mode = e->bit_mode ? 1 : 0;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *pitch)
+{
+    if (!e || !bits || !pitch) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (!e->bit_mode) return gol_set_error(GOL_ESTATE, "board is not bit-resident");
+    *bits = e->bits[e->cur];
+    *pitch = e->pitch;
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------ device launchers
+#define LAUNCH(expr)                                                                                      \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess) return gol_set_error(GOL_EHIP, "%s: %s", #expr, hipGetErrorString(e_));     \
+        return GOL_OK;                                                                                    \
+    } while (0)
+
+extern "C" int gol_dev_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
+                                 int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int32_t k,
+                                 int32_t cells_per_lane, int32_t strip_rows, uint64_t *count_slots, void *stream)
+{
+    const int dw = cells_per_lane > 0 ? cells_per_lane / 32 : GOL_DEFAULT_DW;
+    if (!top || !mid || !bot || !dst || R <= 0 || Wd <= 0 || pitch < Wd || row0 < 0 || rows < 0 ||
+        row0 + rows > R || (dw != 1 && dw != 2 && dw != 4) || Wd % dw || pitch % dw ||
+        !(k == 1 || k == 2 || k == 4 || k == 8 || (k == 16 && dw <= 2)) || k > R)
+        return gol_set_error(GOL_EINVAL, "bad bits_step arguments (R=%lld Wd=%lld pitch=%lld k=%d dw=%d)",
+                             (long long)R, (long long)Wd, (long long)pitch, k, dw);
+    LAUNCH(golk_bits_step(top, mid, bot, dst, R, Wd, pitch, row0, rows, k, dw, strip_rows, count_slots,
+                          (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch,
+                                   uint64_t seed, void *stream)
+{
+    if (!dst || rows < 0 || grow0 < 0 || W <= 0 || W % 64 || pitch < W / 32 || pitch % 2)
+        return gol_set_error(GOL_EINVAL, "bad random_fill arguments");
+    LAUNCH(golk_random_fill(dst, rows, grow0, W, pitch, seed, (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots,
+                                void *stream)
+{
+    if (!src || !slots || rows < 0 || Wd <= 0 || pitch < Wd) return gol_set_error(GOL_EINVAL, "bad popcount arguments");
+    LAUNCH(golk_popcount(src, rows, Wd, pitch, slots, (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_hash(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Wd, int64_t pitch,
+                            uint64_t *slots, void *stream)
+{
+    if (!src || !slots || rows < 0 || grow0 < 0 || Wd <= 0 || Wd % 2 || pitch < Wd || pitch % 2)
+        return gol_set_error(GOL_EINVAL, "bad hash arguments");
+    LAUNCH(golk_hash(src, rows, grow0, Wd, pitch, slots, (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits,
+                            int64_t pitch, uint32_t *nonbinary, void *stream)
+{
+    if (!bytes || !bits || rows < 0 || W <= 0 || W % 32 || stride < W || pitch < W / 32)
+        return gol_set_error(GOL_EINVAL, "bad pack arguments");
+    LAUNCH(golk_pack(bytes, rows, W, stride, bits, pitch, nonbinary, (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes,
+                              int64_t stride, void *stream)
+{
+    if (!bytes || !bits || rows < 0 || W <= 0 || W % 32 || stride < W || pitch < W / 32)
+        return gol_set_error(GOL_EINVAL, "bad unpack arguments");
+    LAUNCH(golk_unpack(bits, rows, W, pitch, bytes, stride, (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0,
+                                  int64_t y1, uint8_t *out, int64_t out_stride, void *stream)
+{
+    if (!world || !out || H <= 0 || W <= 0 || stride < W || out_stride < W || y0 < 0 || y1 > H || y0 > y1)
+        return gol_set_error(GOL_EINVAL, "bad bytes_step arguments");
+    LAUNCH(golk_bytes_step(world, H, W, stride, y0, y1, out, out_stride, (hipStream_t)stream));
+}

@@ -1,0 +1,31 @@
+// gol_kernels.h -- internal launcher interface of gol_kernels.hip (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef GOL_COUNT_SLOTS
+#define GOL_COUNT_SLOTS 256
+#endif
+
+int golk_auto_strip(int64_t rows, int64_t ngroups, int k);
+hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
+                          int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw,
+                          int strip, uint64_t *slots, hipStream_t s);
+hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0, int64_t y1,
+                           uint8_t *out, int64_t out_stride, hipStream_t s);
+hipError_t golk_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch, uint64_t seed,
+                            hipStream_t s);
+hipError_t golk_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots,
+                         hipStream_t s);
+hipError_t golk_hash(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Wd, int64_t pitch, uint64_t *slots,
+                     hipStream_t s);
+hipError_t golk_count_bytes(const uint8_t *src, int64_t rows, int64_t W, int64_t stride, uint64_t *slots,
+                            hipStream_t s);
+hipError_t golk_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits, int64_t pitch,
+                     uint32_t *nonbinary, hipStream_t s);
+hipError_t golk_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes, int64_t stride,
+                       hipStream_t s);
+hipError_t golk_row_counts(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
+                           int64_t *out, hipStream_t s);
+hipError_t golk_alive_list(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
+                           const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s);

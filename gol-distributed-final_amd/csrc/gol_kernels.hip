@@ -1,0 +1,705 @@
+// gol_kernels.hip -- gfx950 (MI355X) kernels of the Game-of-Life hot path.
+//
+// Replaces the reference's per-cell Go loops:
+//   worker.go:15-42 calculateNextState, worker.go:44-70 calculateSurroundings
+//   broker.go:47-58 calculateAliveCells (count part)
+// with two board representations:
+//   * bit board  : 32 cells per uint32 (64 per uint64, LSB = lowest x).  One
+//                  lane owns DW consecutive words of a row and slides down a
+//                  strip of rows; K generations are pipelined in registers
+//                  (temporal blocking), so a launch reads and writes the board
+//                  once for K turns.
+//   * byte board : one byte per cell (exact reference semantics incl. bytes
+//                  that are neither 0 nor 255), SWAR on 4 cells per VGPR.
+// No LDS and no barriers: neighbouring words move between lanes with DPP
+// wave_shr:1 / wave_shl:1; lanes 0 and 63 of every wave are halo lanes whose
+// results are discarded (the halo is one word = 32 cells >= K).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gol_kernels.h"
+
+namespace golk {
+
+// ------------------------------------------------------------------ helpers
+// v_bitop3_b32 truth tables: operand 0 -> 0xF0, operand 1 -> 0xCC, operand 2 -> 0xAA.
+constexpr unsigned TT_XOR3 = 0x96;  // a ^ b ^ c
+constexpr unsigned TT_MAJ = 0xE8;   // majority(a, b, c)
+constexpr unsigned TT_EQ1 = 0x14;   // (a ^ b) & ~c
+constexpr unsigned TT_EQ2 = 0x42;   // c ? ~(a | b) : (a & b)
+constexpr unsigned TT_MUX = 0xCA;   // a ? b : c
+
+template <unsigned TT>
+__device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+}
+// lane i receives lane i-1's value (lane 0 receives 0)
+__device__ __forceinline__ uint32_t from_lower_lane(uint32_t v)
+{
+    return __builtin_amdgcn_mov_dpp(v, 0x138 /* wave_shr:1 */, 0xf, 0xf, true);
+}
+// lane i receives lane i+1's value (lane 63 receives 0)
+__device__ __forceinline__ uint32_t from_upper_lane(uint32_t v)
+{
+    return __builtin_amdgcn_mov_dpp(v, 0x130 /* wave_shl:1 */, 0xf, 0xf, true);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// One atomic per wave into one of GOL_COUNT_SLOTS slots (64 B apart).
+__device__ __forceinline__ void slot_add(uint64_t *slots, uint64_t v)
+{
+    v = wave_sum_u64(v);
+    if ((threadIdx.x & 63) == 0 && v) {
+        unsigned wave = (blockIdx.x + blockIdx.y * gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        atomicAdd((unsigned long long *)&slots[(wave % GOL_COUNT_SLOTS) * 8], (unsigned long long)v);
+    }
+}
+
+template <int DW> struct VecT;
+template <> struct VecT<1> { typedef uint32_t type; };
+template <> struct VecT<2> { typedef uint2 type; };
+template <> struct VecT<4> { typedef uint4 type; };
+
+template <int DW>
+__device__ __forceinline__ void load_words(const uint32_t *p, uint32_t (&w)[DW])
+{
+    typedef typename VecT<DW>::type V;
+    V v = *reinterpret_cast<const V *>(p);
+    if constexpr (DW == 1) { w[0] = v; }
+    if constexpr (DW == 2) { w[0] = v.x; w[1] = v.y; }
+    if constexpr (DW == 4) { w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w; }
+}
+template <int DW>
+__device__ __forceinline__ void store_words(uint32_t *p, const uint32_t (&w)[DW])
+{
+    typedef typename VecT<DW>::type V;
+    V v;
+    if constexpr (DW == 1) { v = w[0]; }
+    if constexpr (DW == 2) { v.x = w[0]; v.y = w[1]; }
+    if constexpr (DW == 4) { v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3]; }
+    *reinterpret_cast<V *>(p) = v;
+}
+
+// Horizontal 3-cell sums of one row (cell itself + left + right), bit-sliced:
+// value = h0 + 2*h1 in 0..3 per cell.
+template <int DW>
+__device__ __forceinline__ void hsum(const uint32_t (&c)[DW], uint32_t (&h0)[DW], uint32_t (&h1)[DW])
+{
+    const uint32_t left_in = from_lower_lane(c[DW - 1]);  // word to the left of c[0]
+    const uint32_t right_in = from_upper_lane(c[0]);      // word to the right of c[DW-1]
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+        const uint32_t wl = (j == 0) ? left_in : c[j - 1];
+        const uint32_t wr = (j == DW - 1) ? right_in : c[j + 1];
+        const uint32_t L = __builtin_amdgcn_alignbit(c[j], wl, 31);  // cell x-1 at bit x
+        const uint32_t R = __builtin_amdgcn_alignbit(wr, c[j], 1);   // cell x+1 at bit x
+        h0[j] = bitop3<TT_XOR3>(L, c[j], R);
+        h1[j] = bitop3<TT_MAJ>(L, c[j], R);
+    }
+}
+
+// B3/S23 from three horizontal sums (rows above/middle/below) and the middle
+// cell.  T = sum of the 3x3 block including the cell = t0 + 2*(k0 + u + 2v);
+// alive' = (T == 3) | (cell & T == 4).
+__device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
+                                         uint32_t c0, uint32_t c1, uint32_t cell)
+{
+    const uint32_t t0 = bitop3<TT_XOR3>(a0, b0, c0);
+    const uint32_t k0 = bitop3<TT_MAJ>(a0, b0, c0);
+    const uint32_t u = bitop3<TT_XOR3>(a1, b1, c1);
+    const uint32_t v = bitop3<TT_MAJ>(a1, b1, c1);
+    const uint32_t eq1 = bitop3<TT_EQ1>(u, k0, v);  // k0 + u + 2v == 1
+    const uint32_t eq2 = bitop3<TT_EQ2>(u, k0, v);  // k0 + u + 2v == 2
+    return bitop3<TT_MUX>(t0, eq1, eq2 & cell);
+}
+
+// ------------------------------------------------------------------ bit-board step
+// Pipeline state of stage g (generation g+1): ring of 3 rows of horizontal sums
+// plus the cells of those rows.  Slot s = step % 3 holds the row received at
+// this step; the stage emits the next state of the row received one step ago.
+template <int K, int DW>
+struct Pipe {
+    uint32_t h0[K][3][DW];
+    uint32_t h1[K][3][DW];
+    uint32_t cc[K][3][DW];
+};
+
+template <int K, int DW, int S>
+__device__ __forceinline__ void pipe_step(Pipe<K, DW> &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+{
+    constexpr int SA = (S + 1) % 3;  // two rows back (above)
+    constexpr int SM = (S + 2) % 3;  // one row back (the row being emitted)
+    uint32_t cur[DW];
+#pragma unroll
+    for (int j = 0; j < DW; ++j) cur[j] = in[j];
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+#pragma unroll
+        for (int j = 0; j < DW; ++j) p.cc[g][S][j] = cur[j];
+        hsum<DW>(p.cc[g][S], p.h0[g][S], p.h1[g][S]);
+#pragma unroll
+        for (int j = 0; j < DW; ++j)
+            cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j],
+                          p.h0[g][S][j], p.h1[g][S][j], p.cc[g][SM][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < DW; ++j) out[j] = cur[j];
+}
+
+struct BitsArgs {
+    const uint32_t *top, *mid, *bot;
+    uint32_t *dst;
+    int64_t R, Wd, pitch, row0, rows;
+    int32_t strip, ngroups;
+    uint64_t *slots;
+};
+
+// grid.x: groups of 4 waves along the row; grid.y: strips of output rows.
+// Wave = one column group of 62*DW output words (+1 halo lane each side).
+template <int K, int DW>
+__global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (group >= a.ngroups) return;  // whole wave exits; no barriers in this kernel
+
+    // column (in words) of this lane's first word, torus-wrapped
+    const int64_t col_raw = (int64_t)group * (62 * DW) + (int64_t)(lane - 1) * DW;
+    const int64_t col = ((col_raw % a.Wd) + a.Wd) % a.Wd;
+    const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
+
+    const int64_t s0 = a.row0 + (int64_t)blockIdx.y * a.strip;             // first output row
+    const int64_t s1 = min(s0 + (int64_t)a.strip, a.row0 + a.rows);         // end output row
+    const int64_t first_in = s0 - K;                                        // first input row
+    const int64_t last_in = s1 + K - 1;                                     // last input row
+    const int64_t nsteps = (s1 - s0) + 2 * K;
+    const int64_t nblk = (nsteps + 2) / 3;
+
+    // Input row y lives at base(y) + y*pitch with base = top + k*pitch (y < 0),
+    // mid (0 <= y < R) or bot - R*pitch (y >= R): scalar pointer + per-lane offset.
+    const uint32_t *top_adj = a.top + K * a.pitch;
+    const uint32_t *bot_adj = a.bot - a.R * a.pitch;
+    const uint32_t lane_off = (uint32_t)col;
+    auto row_ptr = [&](int64_t y) -> const uint32_t * {
+        y = y > last_in ? last_in : y;  // steps past the end re-read the last row; never stored
+        const uint32_t *base = y < 0 ? top_adj : (y >= a.R ? bot_adj : a.mid);
+        return base + y * a.pitch + lane_off;
+    };
+
+    Pipe<K, DW> p;
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int j = 0; j < DW; ++j) { p.h0[g][s][j] = 0; p.h1[g][s][j] = 0; p.cc[g][s][j] = 0; }
+
+    uint32_t buf[3][DW];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + s), buf[s]);
+
+    uint64_t alive = 0;
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        const int64_t t0 = blk * 3;
+        uint32_t nxt[3][DW];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + t0 + 3 + s), nxt[s]);
+
+        uint32_t out[DW];
+#define GOL_STEP(S)                                                                        \
+        {                                                                                  \
+            pipe_step<K, DW, S>(p, buf[S], out);                                           \
+            const int64_t t = t0 + S;                                                      \
+            const int64_t y = s0 + t - 2 * K; /* row emitted by the last stage */          \
+            if (t >= 2 * K && y < s1) {                                                    \
+                if (writer) {                                                              \
+                    store_words<DW>(a.dst + y * a.pitch + col, out);                       \
+                    if (a.slots) {                                                         \
+                        _Pragma("unroll") for (int j = 0; j < DW; ++j) alive += __popc(out[j]); \
+                    }                                                                      \
+                }                                                                          \
+            }                                                                              \
+        }
+        GOL_STEP(0)
+        GOL_STEP(1)
+        GOL_STEP(2)
+#undef GOL_STEP
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int j = 0; j < DW; ++j) buf[s][j] = nxt[s][j];
+    }
+    if (a.slots) slot_add(a.slots, alive);
+}
+
+// ------------------------------------------------------------------ byte-board step (exact semantics)
+// SWAR on 4 cells per uint32.  A = (byte == 255), Z = (byte == 0), as 0x01 per byte.
+__device__ __forceinline__ uint32_t bytes_eq_ff(uint32_t d)
+{
+    const uint32_t x = ~d;
+    const uint32_t nz = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // bit7 set where x byte != 0
+    return (~nz >> 7) & 0x01010101u;
+}
+__device__ __forceinline__ uint32_t bytes_eq_00(uint32_t d)
+{
+    const uint32_t nz = ((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d;
+    return (~nz >> 7) & 0x01010101u;
+}
+
+struct ByteRow {
+    uint32_t a[4];  // (byte == 255) flags
+    uint32_t z[4];  // (byte == 0) flags
+    uint32_t hs[4]; // horizontal 3-sums of the a flags (0..3 per byte)
+};
+
+__device__ __forceinline__ void byte_row(const uint4 v, ByteRow &r)
+{
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { r.a[j] = bytes_eq_ff(d[j]); r.z[j] = bytes_eq_00(d[j]); }
+    const uint32_t left_in = from_lower_lane(r.a[3]);
+    const uint32_t right_in = from_upper_lane(r.a[0]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t wl = j == 0 ? left_in : r.a[j - 1];
+        const uint32_t wr = j == 3 ? right_in : r.a[j + 1];
+        const uint32_t L = __builtin_amdgcn_alignbyte(r.a[j], wl, 3);  // byte x-1 at byte x
+        const uint32_t R = __builtin_amdgcn_alignbyte(wr, r.a[j], 1);  // byte x+1 at byte x
+        r.hs[j] = L + r.a[j] + R;
+    }
+}
+
+__device__ __forceinline__ uint32_t byte_rule(uint32_t hs_up, uint32_t hs_mid, uint32_t hs_dn, uint32_t a,
+                                              uint32_t z)
+{
+    const uint32_t n = hs_up + hs_mid + hs_dn - a;                                   // neighbours, 0..8
+    const uint32_t ne3 = ((n ^ 0x03030303u) + 0x7F7F7F7Fu) & 0x80808080u;           // n != 3
+    const uint32_t ne23 = (((n | 0x01010101u) ^ 0x03030303u) + 0x7F7F7F7Fu) & 0x80808080u;  // n not in {2,3}
+    const uint32_t born = z & ~(ne3 >> 7);
+    const uint32_t surv = a & ~(ne23 >> 7);
+    const uint32_t r = born | surv;  // 0x01 per byte
+    return (r << 8) - r;             // 0xFF per byte
+}
+
+struct BytesArgs {
+    const uint8_t *world;
+    uint8_t *out;
+    int64_t H, W, stride, out_stride, y0, y1;
+    int32_t strip, ngroups;
+};
+
+// Wave = 62 lanes x 16 bytes of output per row; lanes 0/63 are halo.
+__global__ void __launch_bounds__(256) bytes_step_kernel(BytesArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (group >= a.ngroups) return;
+    const int64_t col_raw = (int64_t)group * (62 * 16) + (int64_t)(lane - 1) * 16;
+    const int64_t col = ((col_raw % a.W) + a.W) % a.W;
+    const bool writer = lane >= 1 && lane <= 62 && col_raw < a.W;
+
+    const int64_t s0 = a.y0 + (int64_t)blockIdx.y * a.strip;
+    const int64_t s1 = min(s0 + (int64_t)a.strip, a.y1);
+    auto load = [&](int64_t y) -> uint4 {
+        y = ((y % a.H) + a.H) % a.H;
+        return *reinterpret_cast<const uint4 *>(a.world + y * a.stride + col);
+    };
+    ByteRow up, mid, dn;
+    byte_row(load(s0 - 1), up);
+    byte_row(load(s0), mid);
+    uint4 nxt = load(s0 + 1);
+    for (int64_t y = s0; y < s1; ++y) {
+        byte_row(nxt, dn);
+        nxt = load(y + 2);  // prefetch (wraps harmlessly past the strip)
+        if (writer) {
+            uint4 o;
+            o.x = byte_rule(up.hs[0], mid.hs[0], dn.hs[0], mid.a[0], mid.z[0]);
+            o.y = byte_rule(up.hs[1], mid.hs[1], dn.hs[1], mid.a[1], mid.z[1]);
+            o.z = byte_rule(up.hs[2], mid.hs[2], dn.hs[2], mid.a[2], mid.z[2]);
+            o.w = byte_rule(up.hs[3], mid.hs[3], dn.hs[3], mid.a[3], mid.z[3]);
+            *reinterpret_cast<uint4 *>(a.out + (y - a.y0) * a.out_stride + col) = o;
+        }
+        up = mid;
+        mid = dn;
+    }
+}
+
+// Scalar fallback for widths that are not a multiple of 16 (one thread per cell),
+// a literal restatement of worker.go:26-37 / 44-70.
+__global__ void bytes_step_scalar_kernel(BytesArgs a)
+{
+    const int64_t n = (a.y1 - a.y0) * a.W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = a.y0 + i / a.W, x = i % a.W;
+        const int64_t ya = (y + a.H - 1) % a.H, yb = (y + 1) % a.H;
+        const int64_t xl = (x + a.W - 1) % a.W, xr = (x + 1) % a.W;
+        const uint8_t *w = a.world;
+        const int64_t s = a.stride;
+        int cnt = (w[ya * s + xl] == 255) + (w[ya * s + x] == 255) + (w[ya * s + xr] == 255) +
+                  (w[y * s + xl] == 255) + (w[y * s + xr] == 255) + (w[yb * s + xl] == 255) +
+                  (w[yb * s + x] == 255) + (w[yb * s + xr] == 255);
+        const uint8_t c = w[y * s + x];
+        uint8_t o = 0;
+        if (c == 0 && cnt == 3) o = 255;
+        if (c == 255 && (cnt == 2 || cnt == 3)) o = 255;
+        a.out[(y - a.y0) * a.out_stride + x] = o;
+    }
+}
+
+// ------------------------------------------------------------------ board utilities
+// Synthetic board: 64-bit word (y, w) = splitmix64(seed ^ (y*Ww + w)).
+__global__ void random_fill_kernel(uint32_t *dst, int64_t rows, int64_t grow0, int64_t Ww, int64_t pitch,
+                                   uint64_t seed)
+{
+    const int64_t n = rows * Ww;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / Ww, w = i % Ww;
+        const uint64_t v = splitmix64(seed ^ (uint64_t)((grow0 + y) * Ww + w));
+        *reinterpret_cast<uint2 *>(dst + y * pitch + 2 * w) = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+    }
+}
+
+__global__ void popcount_kernel(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots)
+{
+    uint64_t c = 0;
+    const int64_t n = rows * Wd;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / Wd, w = i % Wd;
+        c += __popc(src[y * pitch + w]);
+    }
+    slot_add(slots, c);
+}
+
+__global__ void hash_kernel(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Ww, int64_t pitch,
+                            uint64_t *slots)
+{
+    uint64_t h = 0;
+    const int64_t n = rows * Ww;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / Ww, w = i % Ww;
+        const uint2 v = *reinterpret_cast<const uint2 *>(src + y * pitch + 2 * w);
+        const uint64_t word = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        h += splitmix64(word ^ splitmix64((uint64_t)((grow0 + y) * Ww + w)));
+    }
+    slot_add(slots, h);
+}
+
+__global__ void count_nonzero_bytes_kernel(const uint8_t *src, int64_t rows, int64_t W, int64_t stride,
+                                           uint64_t *slots)
+{
+    uint64_t c = 0;
+    const int64_t n = rows * W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / W, x = i % W;
+        c += src[y * stride + x] != 0;
+    }
+    slot_add(slots, c);
+}
+
+// bytes -> bits: one thread per 32-cell word
+__global__ void pack_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits,
+                            int64_t pitch, uint32_t *nonbinary)
+{
+    const int64_t Wd = W / 32;
+    const int64_t n = rows * Wd;
+    uint32_t bad = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / Wd, w = i % Wd;
+        const uint8_t *p = bytes + y * stride + 32 * w;
+        uint32_t v = 0;
+#pragma unroll 8
+        for (int b = 0; b < 32; ++b) {
+            const uint8_t c = p[b];
+            v |= (uint32_t)(c == 255) << b;
+            bad |= (c != 0 && c != 255);
+        }
+        bits[y * pitch + w] = v;
+    }
+    if (nonbinary && bad) atomicOr(nonbinary, 1u);
+}
+
+// bits -> bytes (0/255): one thread per 32-cell word, two 16-byte stores
+__global__ void unpack_kernel(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes,
+                              int64_t stride)
+{
+    const int64_t Wd = W / 32;
+    const int64_t n = rows * Wd;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / Wd, w = i % Wd;
+        const uint32_t v = bits[y * pitch + w];
+        uint32_t o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t nib = (v >> (4 * q)) & 0xF;
+            // spread 4 bits to 4 bytes, then 0x01 -> 0xFF
+            const uint32_t s = (nib & 1) | ((nib & 2) << 7) | ((nib & 4) << 14) | ((nib & 8) << 21);
+            o[q] = (s << 8) - s;
+        }
+        uint8_t *dst = bytes + y * stride + 32 * w;
+        if (((uintptr_t)dst & 15) == 0) {
+            reinterpret_cast<uint4 *>(dst)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+            reinterpret_cast<uint4 *>(dst)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+        } else {
+            for (int q = 0; q < 8; ++q)
+                for (int b = 0; b < 4; ++b) dst[4 * q + b] = (uint8_t)(o[q] >> (8 * b));
+        }
+    }
+}
+
+// Alive-cell list, row-major (broker.go:47-58): one wave per row, ballot + mbcnt
+// prefix over 64 cells at a time.  offs[y] = first output index of row y.
+__global__ void alive_list_bits_kernel(const uint32_t *bits, int64_t rows, int64_t Wd, int64_t pitch,
+                                       const int64_t *offs, int32_t *xy, int64_t cap)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (y >= rows) return;
+    int64_t base = offs[y];
+    for (int64_t w0 = 0; w0 < Wd; w0 += 64) {
+        const int64_t w = w0 + lane;
+        const uint32_t v = w < Wd ? bits[y * pitch + w] : 0u;
+        const uint32_t c = __popc(v);
+        // exclusive prefix of c over the wave
+        uint32_t incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+        }
+        int64_t o = base + (incl - c);
+        uint32_t m = v;
+        while (m) {
+            const int b = __ffs(m) - 1;
+            m &= m - 1;
+            if (o < cap) { xy[2 * o] = (int32_t)(32 * w + b); xy[2 * o + 1] = (int32_t)y; }
+            ++o;
+        }
+        base += __shfl(incl, 63, 64);
+    }
+}
+
+__global__ void alive_list_bytes_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride,
+                                        const int64_t *offs, int32_t *xy, int64_t cap)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (y >= rows) return;
+    int64_t base = offs[y];
+    for (int64_t x0 = 0; x0 < W; x0 += 64) {
+        const int64_t x = x0 + lane;
+        const bool alive = x < W && bytes[y * stride + x] != 0;
+        const uint64_t m = __ballot(alive);
+        if (alive) {
+            const int64_t o = base + __popcll(m & ((1ULL << lane) - 1));
+            if (o < cap) { xy[2 * o] = (int32_t)x; xy[2 * o + 1] = (int32_t)y; }
+        }
+        base += __popcll(m);
+    }
+}
+
+__global__ void row_counts_bits_kernel(const uint32_t *bits, int64_t rows, int64_t Wd, int64_t pitch, int64_t *out)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (y >= rows) return;
+    uint64_t c = 0;
+    for (int64_t w = lane; w < Wd; w += 64) c += __popc(bits[y * pitch + w]);
+    c = wave_sum_u64(c);
+    if (lane == 0) out[y] = (int64_t)c;
+}
+
+__global__ void row_counts_bytes_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, int64_t *out)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (y >= rows) return;
+    uint64_t c = 0;
+    for (int64_t x = lane; x < W; x += 64) c += bytes[y * stride + x] != 0;
+    c = wave_sum_u64(c);
+    if (lane == 0) out[y] = (int64_t)c;
+}
+
+}  // namespace golk
+
+// ------------------------------------------------------------------ launchers
+using namespace golk;
+
+static inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 16)
+{
+    int64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+template <int K, int DW>
+static hipError_t launch_bits(const BitsArgs &a, hipStream_t s)
+{
+    const int nstrips = (int)((a.rows + a.strip - 1) / a.strip);
+    dim3 grid((a.ngroups + 3) / 4, nstrips);
+    hipLaunchKernelGGL((bits_step_kernel<K, DW>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int DW>
+static hipError_t launch_bits_k(int k, const BitsArgs &a, hipStream_t s)
+{
+    switch (k) {
+    case 1: return launch_bits<1, DW>(a, s);
+    case 2: return launch_bits<2, DW>(a, s);
+    case 4: return launch_bits<4, DW>(a, s);
+    case 8: return launch_bits<8, DW>(a, s);
+    case 16: if constexpr (DW <= 2) return launch_bits<16, DW>(a, s);
+             return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+    }
+}
+
+int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
+{
+    // aim for >= ~8192 waves (32 per CU) while keeping the 2k halo rows small
+    int64_t strip = rows * ngroups / 8192;
+    if (strip > 1024) strip = 1024;
+    int64_t lo = 8 * (int64_t)k;
+    if (lo < 32) lo = 32;
+    if (strip < lo) strip = lo;
+    if (strip > rows) strip = rows;
+    if (strip < 1) strip = 1;
+    return (int)strip;
+}
+
+hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
+                          int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw,
+                          int strip, uint64_t *slots, hipStream_t s)
+{
+    BitsArgs a;
+    a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
+    a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
+    a.ngroups = (int)((Wd + 62 * dw - 1) / (62 * dw));
+    a.strip = strip > 0 ? strip : golk_auto_strip(rows, a.ngroups, k);
+    a.slots = slots;
+    if (rows <= 0) return hipSuccess;
+    switch (dw) {
+    case 1: return launch_bits_k<1>(k, a, s);
+    case 2: return launch_bits_k<2>(k, a, s);
+    case 4: return launch_bits_k<4>(k, a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0, int64_t y1,
+                           uint8_t *out, int64_t out_stride, hipStream_t s)
+{
+    BytesArgs a;
+    a.world = world; a.out = out; a.H = H; a.W = W; a.stride = stride; a.out_stride = out_stride;
+    a.y0 = y0; a.y1 = y1;
+    if (y1 <= y0) return hipSuccess;
+    const bool vec = (W % 16 == 0) && (stride % 16 == 0) && (out_stride % 16 == 0) &&
+                     (((uintptr_t)world & 15) == 0) && (((uintptr_t)out & 15) == 0);
+    if (vec) {
+        a.ngroups = (int)((W + 62 * 16 - 1) / (62 * 16));
+        const int64_t rows = y1 - y0;
+        int64_t strip = rows * a.ngroups / 8192;
+        if (strip < 16) strip = 16;
+        if (strip > 256) strip = 256;
+        if (strip > rows) strip = rows;
+        a.strip = (int)strip;
+        dim3 grid((a.ngroups + 3) / 4, (int)((rows + strip - 1) / strip));
+        hipLaunchKernelGGL(bytes_step_kernel, grid, dim3(256), 0, s, a);
+    } else {
+        a.ngroups = 0; a.strip = 0;
+        hipLaunchKernelGGL(bytes_step_scalar_kernel, dim3(grid_for((y1 - y0) * W)), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t golk_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch, uint64_t seed,
+                            hipStream_t s)
+{
+    const int64_t Ww = W / 64;
+    hipLaunchKernelGGL(random_fill_kernel, dim3(grid_for(rows * Ww, 256, 256 * 64)), dim3(256), 0, s, dst, rows,
+                       grow0, Ww, pitch, seed);
+    return hipGetLastError();
+}
+
+hipError_t golk_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots, hipStream_t s)
+{
+    hipLaunchKernelGGL(popcount_kernel, dim3(grid_for(rows * Wd, 256, 256 * 16)), dim3(256), 0, s, src, rows, Wd,
+                       pitch, slots);
+    return hipGetLastError();
+}
+
+hipError_t golk_hash(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Wd, int64_t pitch, uint64_t *slots,
+                     hipStream_t s)
+{
+    hipLaunchKernelGGL(hash_kernel, dim3(grid_for(rows * (Wd / 2), 256, 256 * 16)), dim3(256), 0, s, src, rows,
+                       grow0, Wd / 2, pitch, slots);
+    return hipGetLastError();
+}
+
+hipError_t golk_count_bytes(const uint8_t *src, int64_t rows, int64_t W, int64_t stride, uint64_t *slots,
+                            hipStream_t s)
+{
+    hipLaunchKernelGGL(count_nonzero_bytes_kernel, dim3(grid_for(rows * W, 256, 256 * 16)), dim3(256), 0, s, src,
+                       rows, W, stride, slots);
+    return hipGetLastError();
+}
+
+hipError_t golk_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits, int64_t pitch,
+                     uint32_t *nonbinary, hipStream_t s)
+{
+    hipLaunchKernelGGL(pack_kernel, dim3(grid_for(rows * (W / 32), 256, 256 * 64)), dim3(256), 0, s, bytes, rows, W,
+                       stride, bits, pitch, nonbinary);
+    return hipGetLastError();
+}
+
+hipError_t golk_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes, int64_t stride,
+                       hipStream_t s)
+{
+    hipLaunchKernelGGL(unpack_kernel, dim3(grid_for(rows * (W / 32), 256, 256 * 64)), dim3(256), 0, s, bits, rows, W,
+                       pitch, bytes, stride);
+    return hipGetLastError();
+}
+
+hipError_t golk_row_counts(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
+                           int64_t *out, hipStream_t s)
+{
+    const int wpb = 4;
+    dim3 grid((unsigned)((rows + wpb - 1) / wpb));
+    if (bits_mode)
+        hipLaunchKernelGGL(row_counts_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board, rows,
+                           width_units, pitch, out);
+    else
+        hipLaunchKernelGGL(row_counts_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board, rows,
+                           width_units, pitch, out);
+    return hipGetLastError();
+}
+
+hipError_t golk_alive_list(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
+                           const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s)
+{
+    const int wpb = 4;
+    dim3 grid((unsigned)((rows + wpb - 1) / wpb));
+    if (bits_mode)
+        hipLaunchKernelGGL(alive_list_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board, rows,
+                           width_units, pitch, offs, xy, cap);
+    else
+        hipLaunchKernelGGL(alive_list_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board, rows,
+                           width_units, pitch, offs, xy, cap);
+    return hipGetLastError();
+}

@@ -1,0 +1,130 @@
+"""ctypes binding of libgolhip.so (include/golhip.h).
+
+The library is the product: it is built in-tree by ``__graft_entry__.build()``
+(hipcc, gfx950) next to this file.  There is no fallback -- if the shared
+object is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgolhip.so")
+
+GOL_OK = 0
+GOL_EINVAL = -1
+GOL_EHIP = -2
+GOL_ENOMEM = -3
+GOL_EIO = -4
+GOL_EFORMAT = -5
+GOL_ESTATE = -6
+GOL_EQUIT = -7
+GOL_COUNT_SLOTS = 256
+
+_NAMES = {
+    GOL_EINVAL: "EINVAL", GOL_EHIP: "EHIP", GOL_ENOMEM: "ENOMEM", GOL_EIO: "EIO",
+    GOL_EFORMAT: "EFORMAT", GOL_ESTATE: "ESTATE", GOL_EQUIT: "EQUIT",
+}
+
+
+class GolError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+class gol_config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
+                ("strip_rows", ctypes.c_int32), ("cells_per_lane", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 4)]
+
+
+class gol_request(ctypes.Structure):
+    _fields_ = [("World", ctypes.c_void_p), ("world_stride", ctypes.c_int64),
+                ("Turns", ctypes.c_int64), ("ImageHeight", ctypes.c_int64),
+                ("ImageWidth", ctypes.c_int64), ("Threads", ctypes.c_int64),
+                ("EndY", ctypes.c_int64), ("StartY", ctypes.c_int64), ("Worker", ctypes.c_int64)]
+
+
+class gol_response(ctypes.Structure):
+    _fields_ = [("Alive", ctypes.c_void_p), ("alive_cap", ctypes.c_int64),
+                ("alive_len", ctypes.c_int64), ("AliveCount", ctypes.c_int64),
+                ("TurnsCompleted", ctypes.c_int64), ("World", ctypes.c_void_p),
+                ("world_stride", ctypes.c_int64), ("WorkSlice", ctypes.c_void_p),
+                ("work_stride", ctypes.c_int64), ("Worker", ctypes.c_int64)]
+
+
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_u64 = ctypes.c_uint64
+_vp = ctypes.c_void_p
+_P = ctypes.POINTER
+
+# (name, restype, argtypes) -- one row per declaration in include/golhip.h
+SIGNATURES = [
+    ("gol_abi_version", ctypes.c_int, []),
+    ("gol_last_error", ctypes.c_char_p, []),
+    ("gol_device_count", ctypes.c_int, [_P(ctypes.c_int)]),
+    ("gol_next_state_slab", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64]),
+    ("gol_partition_rows", ctypes.c_int, [_i64, _i64, _i64, _P(_i64), _P(_i64)]),
+    ("gol_engine_create", ctypes.c_int, [_i64, _i64, _P(gol_config), _P(_vp)]),
+    ("gol_engine_destroy", None, [_vp]),
+    ("gol_engine_load_bytes", ctypes.c_int, [_vp, _vp, _i64]),
+    ("gol_engine_load_random", ctypes.c_int, [_vp, _u64]),
+    ("gol_engine_step", ctypes.c_int, [_vp, _i64]),
+    ("gol_engine_turn", ctypes.c_int, [_vp, _P(_i64)]),
+    ("gol_engine_alive_count", ctypes.c_int, [_vp, _P(_u64)]),
+    ("gol_engine_store_bytes", ctypes.c_int, [_vp, _vp, _i64]),
+    ("gol_engine_alive_cells", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
+    ("gol_engine_write_pgm", ctypes.c_int, [_vp, ctypes.c_char_p]),
+    ("gol_engine_hash", ctypes.c_int, [_vp, _P(_u64)]),
+    ("gol_engine_info", ctypes.c_int, [_vp, _P(_i32), _P(_i32), _P(_i32), _P(_i32)]),
+    ("gol_engine_device_bits", ctypes.c_int, [_vp, _P(_vp), _P(_i64)]),
+    ("gol_dev_bits_step", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
+    ("gol_dev_random_fill", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _u64, _vp]),
+    ("gol_dev_popcount", ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp]),
+    ("gol_dev_hash", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp]),
+    ("gol_dev_pack", ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
+    ("gol_dev_unpack", ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
+    ("gol_dev_bytes_step", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp]),
+    ("gol_broker_create", ctypes.c_int, [_P(gol_config), _P(_vp)]),
+    ("gol_broker_destroy", None, [_vp]),
+    ("gol_broker_run", ctypes.c_int, [_vp, _P(gol_request), _P(gol_response)]),
+    ("gol_broker_retrieve", ctypes.c_int, [_vp, _P(gol_request), _P(gol_response)]),
+    ("gol_broker_pause", ctypes.c_int, [_vp]),
+    ("gol_broker_quit", ctypes.c_int, [_vp]),
+    ("gol_broker_superquit", ctypes.c_int, [_vp]),
+    ("gol_broker_paused", ctypes.c_int, [_vp, _P(_i32)]),
+    ("gol_worker_update", ctypes.c_int, [_P(gol_request), _P(gol_response)]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libgolhip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GolError(GOL_ESTATE, f"{LIB_PATH} is missing: run __graft_entry__.build() "
+                                       "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != GOL_OK:
+        raise GolError(rc, lib().gol_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    check(lib().gol_device_count(ctypes.byref(n)))
+    return n.value

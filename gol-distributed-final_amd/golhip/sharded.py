@@ -1,0 +1,218 @@
+"""Row-sharded Game-of-Life torus over several MI355X, one process per GPU.
+
+The reference splits the board into `Threads` row slabs per turn and ships the
+WHOLE board to every worker each turn (broker.go:135-206, 143-157).  Here the
+same partition (gol_partition_rows, broker.go:172-206) is applied once to GPUs:
+rank r keeps rows [y0_r, y1_r) bit-packed in its own HBM for the whole run.
+Every k turns the only traffic is a k-row halo with each ring neighbour,
+exchanged with torch.distributed point-to-point ops (backend "nccl" = RCCL
+over xGMI on MI355X) while the interior rows are computed:
+
+    isend(my top k rows -> rank-1)   irecv(bottom halo <- rank+1)
+    isend(my bottom k rows -> rank+1) irecv(top halo   <- rank-1)
+    interior launch: output rows [k, R-k)      (needs no halo; overlaps the exchange)
+    wait; boundary launches: rows [0, k) and [R-k, R)
+
+With one rank there is no exchange: the kernel reads the torus wrap directly.
+Counts and hashes are per-shard reductions summed with one all_reduce.
+PyTorch provides device memory, the stream and torch.distributed only; all
+board arithmetic runs in libgolhip.so's gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from ._lib import GOL_COUNT_SLOTS, check, lib
+from .engine import partition_rows
+
+VALID_K = (16, 8, 4, 2, 1)
+
+
+class HipKernels:
+    """Launch the C-ABI device kernels on torch CUDA tensors and torch's current stream."""
+
+    def __init__(self, cells_per_lane: int = 0, strip_rows: int = 0):
+        self.cells_per_lane = cells_per_lane
+        self.strip_rows = strip_rows
+        lib()  # fail loudly now if the library is missing
+
+    @staticmethod
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def bits_step(self, top, mid, bot, dst, row0: int, rows: int, k: int, slots=None) -> None:
+        R, pitch = mid.shape
+        check(lib().gol_dev_bits_step(top.data_ptr(), mid.data_ptr(), bot.data_ptr(), dst.data_ptr(), R,
+                                      self.Wd, pitch, row0, rows, k, self.cells_per_lane, self.strip_rows,
+                                      slots.data_ptr() if slots is not None else None, self._stream()))
+
+    def random_fill(self, dst, grow0: int, W: int, seed: int) -> None:
+        rows, pitch = dst.shape
+        check(lib().gol_dev_random_fill(dst.data_ptr(), rows, grow0, W, pitch, seed, self._stream()))
+
+    def popcount(self, src, slots) -> None:
+        rows, pitch = src.shape
+        check(lib().gol_dev_popcount(src.data_ptr(), rows, self.Wd, pitch, slots.data_ptr(), self._stream()))
+
+    def hash(self, src, grow0: int, slots) -> None:
+        rows, pitch = src.shape
+        check(lib().gol_dev_hash(src.data_ptr(), rows, grow0, self.Wd, pitch, slots.data_ptr(), self._stream()))
+
+    def unpack(self, src, W: int) -> torch.Tensor:
+        rows, pitch = src.shape
+        out = torch.empty((rows, W), dtype=torch.uint8, device=src.device)
+        check(lib().gol_dev_unpack(src.data_ptr(), rows, W, pitch, out.data_ptr(), W, self._stream()))
+        return out
+
+    def pack(self, board, dst) -> None:
+        rows, W = board.shape
+        check(lib().gol_dev_pack(board.data_ptr(), rows, W, W, dst.data_ptr(), dst.shape[1], None,
+                                 self._stream()))
+
+
+class ShardedBoard:
+    """A W-wide, H-tall bit-packed torus, rows sharded over the ranks of `group`."""
+
+    def __init__(self, height: int, width: int, *, turns_per_launch: int = 8, cells_per_lane: int = 0,
+                 strip_rows: int = 0, device=None, kernels=None, group=None):
+        if width % 64:
+            raise ValueError("the sharded bit board needs W % 64 == 0")
+        self.H, self.W = int(height), int(width)
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank, self.nranks = dist.get_rank(group), dist.get_world_size(group)
+        else:
+            self.rank, self.nranks = 0, 1
+        self.y0, self.y1 = partition_rows(self.H, self.nranks, self.rank)
+        self.R = self.y1 - self.y0
+        min_rows = self.H // self.nranks  # smallest shard (broker.go:172-206 split)
+        if min_rows < 1:
+            raise ValueError(f"{self.nranks} ranks cannot shard {self.H} rows")
+        self.kmax = max(k for k in VALID_K if k <= max(1, min(turns_per_launch, min_rows)))
+        self.Wd = self.W // 32
+        self.pitch = (self.Wd + 3) // 4 * 4
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if kernels is None else torch.device("cpu")
+        self.device = torch.device(device)
+        self.kern = kernels if kernels is not None else HipKernels(cells_per_lane, strip_rows)
+        self.kern.Wd = self.Wd
+        z = dict(dtype=torch.int32, device=self.device)
+        self.buf = [torch.zeros((self.R, self.pitch), **z), torch.zeros((self.R, self.pitch), **z)]
+        self.cur = 0
+        self.ghost_top = torch.zeros((self.kmax, self.pitch), **z)
+        self.ghost_bot = torch.zeros((self.kmax, self.pitch), **z)
+        self.slots = torch.zeros(GOL_COUNT_SLOTS * 8, dtype=torch.int64, device=self.device)
+        self.turn = 0
+        self.prev = (self.rank - 1) % self.nranks
+        self.next = (self.rank + 1) % self.nranks
+        # per-launch timing hooks for bench.py: called as hook("interior"|"boundary"|"full", k, rows)
+        self.launch_hook = None
+
+    # ------------------------------------------------------------ board in/out
+    @property
+    def board(self) -> torch.Tensor:
+        return self.buf[self.cur]
+
+    def load_random(self, seed: int) -> None:
+        """Synthetic torus: identical global board for every rank count."""
+        self.kern.random_fill(self.board, self.y0, self.W, seed)
+        self.turn = 0
+
+    def load_bytes(self, board_rows) -> None:
+        """Load this rank's rows [y0, y1) from a (R, W) uint8 tensor of 0/255 bytes."""
+        if tuple(board_rows.shape) != (self.R, self.W):
+            raise ValueError("expected this rank's (R, W) rows")
+        self.kern.pack(board_rows.to(self.device).contiguous(), self.board)
+        self.turn = 0
+
+    # ------------------------------------------------------------ stepping
+    def _exchange(self, k: int):
+        cur = self.board
+        if self.nranks == 1:
+            return None
+        g = self.group
+        ops = [dist.P2POp(dist.isend, cur[:k], self.prev, g),
+               dist.P2POp(dist.irecv, self.ghost_bot[:k], self.next, g),
+               dist.P2POp(dist.isend, cur[self.R - k:], self.next, g),
+               dist.P2POp(dist.irecv, self.ghost_top[:k], self.prev, g)]
+        return dist.batch_isend_irecv(ops)
+
+    def _launch(self, kind, top, bot, dst, row0, rows, k, slots):
+        if rows <= 0:
+            return
+        hook = self.launch_hook
+        if hook is not None:
+            hook(kind, k, rows, True)
+        self.kern.bits_step(top, self.board, bot, dst, row0, rows, k, slots)
+        if hook is not None:
+            hook(kind, k, rows, False)
+
+    def step(self, turns: int, count: bool = False) -> None:
+        """Advance exactly `turns` turns (k-turn launches + halo exchange)."""
+        while turns > 0:
+            k = max(kk for kk in VALID_K if kk <= min(self.kmax, turns))
+            last = turns == k
+            slots = self.slots if (count and last) else None
+            if slots is not None:
+                slots.zero_()
+            cur, dst = self.board, self.buf[1 - self.cur]
+            R = self.R
+            if self.nranks == 1:
+                self._launch("full", cur[R - k:], cur, dst, 0, R, k, slots)
+            else:
+                reqs = self._exchange(k)
+                interior = R >= 3 * k
+                if interior:
+                    self._launch("interior", self.ghost_top, self.ghost_bot, dst, k, R - 2 * k, k, slots)
+                for r in reqs:
+                    r.wait()
+                if interior:
+                    self._launch("boundary", self.ghost_top, self.ghost_bot, dst, 0, k, k, slots)
+                    self._launch("boundary", self.ghost_top, self.ghost_bot, dst, R - k, k, k, slots)
+                else:
+                    self._launch("boundary", self.ghost_top, self.ghost_bot, dst, 0, R, k, slots)
+            self.cur = 1 - self.cur
+            self.turn += k
+            turns -= k
+
+    # ------------------------------------------------------------ queries
+    def _allreduce(self, t: torch.Tensor) -> int:
+        if self.nranks > 1:
+            dist.all_reduce(t, group=self.group)
+        return int(t.item()) & (2**64 - 1)
+
+    def _slot_sum(self) -> torch.Tensor:
+        return self.slots.view(GOL_COUNT_SLOTS, 8)[:, 0].sum().reshape(1)
+
+    def alive_count(self) -> int:
+        self.slots.zero_()
+        self.kern.popcount(self.board, self.slots)
+        return self._allreduce(self._slot_sum())
+
+    def fused_count(self) -> int:
+        """Alive count accumulated by the last launch of the last step(count=True)."""
+        return self._allreduce(self._slot_sum())
+
+    def hash(self) -> int:
+        """Order-independent board hash (oracle_hash_words), summed over shards."""
+        self.slots.zero_()
+        self.kern.hash(self.board, self.y0, self.slots)
+        return self._allreduce(self._slot_sum())
+
+    def gather_bytes(self):
+        """Whole board as (H, W) uint8 0/255 on rank 0 (None elsewhere).  Small boards only."""
+        mine = self.kern.unpack(self.board, self.W)
+        if self.nranks == 1:
+            return mine.cpu()
+        parts = [torch.empty((partition_rows(self.H, self.nranks, r)[1] - partition_rows(self.H, self.nranks, r)[0],
+                              self.W), dtype=torch.uint8, device=mine.device) for r in range(self.nranks)]
+        if self.rank == 0:
+            parts[0].copy_(mine)
+            for r in range(1, self.nranks):
+                dist.recv(parts[r], r, group=self.group)
+            return torch.cat([p.cpu() for p in parts])
+        dist.send(mine, 0, group=self.group)
+        return None

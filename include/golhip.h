@@ -1,0 +1,206 @@
+/*
+ * golhip.h -- C ABI of libgolhip.so, the MI355X (gfx950) Game-of-Life hot path.
+ *
+ * The reference (ao22174/Gol-distributed-final) is Go; its hot path is reached
+ * over net/rpc.  This ABI is what a cgo binding of that path would bind (the
+ * stub is in INTEGRATION.md).  Every entry point names the reference
+ * interface it replaces (file:line inside the reference tree).
+ *
+ * Conventions
+ *  - Every call returns an int status: GOL_OK (0) or a negative GOL_E* code.
+ *    It never aborts the process.  gol_last_error() gives a thread-local
+ *    message for the last failing call on the calling thread.  (The
+ *    reference panics on local failures, util/check.go:3-7, and its RPC
+ *    handlers always return nil; a Go host maps nonzero codes to `error`.)
+ *  - Host buffers are caller-owned and only borrowed for the duration of a
+ *    call; the library never retains a host pointer.  Device memory created
+ *    by an engine is engine-owned and released by gol_engine_destroy.
+ *  - Boards: byte boards are row-major [y][x], one byte per cell, 255 = alive,
+ *    0 = dead (README.md:25-32); `stride` is the row pitch in bytes.
+ *    Bit boards are row-major, 64 cells per uint64 (LSB = lowest x), i.e. 32
+ *    cells per uint32 little-endian; `pitch` is the row pitch in uint32 words.
+ *  - Torus semantics: rows wrap with H, columns with W.  The reference wraps
+ *    both axes with len(world[0]) (worker.go:48-59) and is only defined for
+ *    square boards, where the two agree.
+ *  - Thread safety: gol_next_state_slab and the gol_dev_* launchers are
+ *    re-entrant.  A gol_engine handle is not internally synchronised; callers
+ *    serialise access (the broker mirror does, like broker.go's `mt`).
+ */
+#ifndef GOLHIP_H
+#define GOLHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOL_ABI_VERSION 1
+
+enum {
+    GOL_OK = 0,
+    GOL_EINVAL = -1,   /* bad argument */
+    GOL_EHIP = -2,     /* HIP runtime error */
+    GOL_ENOMEM = -3,   /* allocation failed */
+    GOL_EIO = -4,      /* file I/O */
+    GOL_EFORMAT = -5,  /* malformed PGM (io.go:101-117 panics) */
+    GOL_ESTATE = -6,   /* call not valid in the current state */
+    GOL_EQUIT = -7     /* broker was shut down (SuperQuit) */
+};
+
+/* ---------------------------------------------------------------- library */
+int gol_abi_version(void);
+const char *gol_last_error(void);
+int gol_device_count(int *n);
+
+/* ---------------------------------------------------------------- worker path
+ * Replaces worker.go:15-42 calculateNextState + worker.go:44-70
+ * calculateSurroundings, as called by GameOfLifeOperations.Update
+ * (worker.go:77-80).  Exact reference semantics per byte: a cell that is
+ * exactly 0 with exactly 3 neighbours equal to 255 becomes 255; a cell equal to
+ * 255 with 2 or 3 such neighbours stays 255; every other cell becomes 0.
+ * world: H x W bytes (row pitch `stride`); out: (y1-y0) x W bytes (pitch
+ * out_stride) = next state of rows [y0, y1).  Runs on the current device. */
+int gol_next_state_slab(const uint8_t *world, int64_t H, int64_t W, int64_t stride,
+                        int64_t y0, int64_t y1, uint8_t *out, int64_t out_stride);
+
+/* Replaces the row split of broker.go:135-139 (H % T == 0: StartY = i*H/T,
+ * EndY = (i+1)*H/T) and broker.go:172-206 (else the first H % T slabs get
+ * H/T + 1 rows, the rest H/T, in order).  Also used to row-shard a board over
+ * GPUs. */
+int gol_partition_rows(int64_t H, int64_t parts, int64_t i, int64_t *y0, int64_t *y1);
+
+/* ---------------------------------------------------------------- engine
+ * A board resident on one GPU.  Replaces the broker's per-turn state
+ * (`world`, `cWorld`, `cTurn`: broker.go:22-36, 62-234) and the per-turn
+ * scatter/gather to workers (broker.go:143-157, 182-211): the board stays in
+ * HBM and is stepped in k-turn launches. */
+typedef struct gol_engine gol_engine;
+
+typedef struct gol_config {
+    int32_t device;           /* HIP device ordinal; -1 = current device */
+    int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
+    int32_t strip_rows;       /* rows per wave strip; 0 = automatic */
+    int32_t cells_per_lane;   /* 32, 64 or 128 bits per lane; 0 = automatic */
+    int32_t reserved[4];
+} gol_config;
+
+int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, gol_engine **out);
+void gol_engine_destroy(gol_engine *e);
+/* Load a byte board (operations.Run's req.World, broker.go:65) and reset the
+ * turn counter to 0.  Any byte value is accepted (exact semantics above). */
+int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_t stride);
+/* Synthetic board: word(y, w) = splitmix64(seed ^ (y*W/64 + w)), Bernoulli(1/2)
+ * per cell (W % 64 == 0 only).  Resets the turn counter. */
+int gol_engine_load_random(gol_engine *e, uint64_t seed);
+/* Advance exactly `turns` turns (blocking).  Replaces the turn loop body of
+ * broker.go:75-226. */
+int gol_engine_step(gol_engine *e, int64_t turns);
+int gol_engine_turn(gol_engine *e, int64_t *turn);
+/* Number of cells != 0 -- len(calculateAliveCells(...)), broker.go:273. */
+int gol_engine_alive_count(gol_engine *e, uint64_t *count);
+/* Copy the board out as bytes (0/255, or the loaded bytes before turn 1). */
+int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t stride);
+/* calculateAliveCells (broker.go:47-58): (x, y) int32 pairs in row-major
+ * order; writes min(n, cap) pairs, *n = total alive cells. */
+int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n);
+/* writePgmImage byte stream (gol/io.go:52-81): "P5\n<W> <H>\n255\n" + H*W
+ * bytes, streamed from the device in chunks. */
+int gol_engine_write_pgm(gol_engine *e, const char *path);
+/* Order-independent board hash (same definition as oracle_hash_words):
+ * sum over 64-bit words of splitmix64(word ^ splitmix64(y*W/64 + w)).
+ * W % 64 == 0 only. */
+int gol_engine_hash(gol_engine *e, uint64_t *hash);
+/* Chosen kernel parameters (k, cells per lane, strip rows, resident mode: 0 =
+ * byte board, 1 = bit board). */
+int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lane, int32_t *strip_rows,
+                    int32_t *bit_mode);
+/* Raw device pointer to the current bit board (pitch in uint32 words), for
+ * tests and the PGM snapshot of a sharded board. */
+int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *pitch);
+
+/* ---------------------------------------------------------------- device launchers
+ * Asynchronous kernel launches on caller-owned device memory and a caller
+ * stream (hipStream_t passed as void*; NULL = default stream).  These are the
+ * building blocks of the row-sharded multi-GPU board (one process per GPU;
+ * broker.go:135-206's partition applied to GPUs) and of bench.py.
+ *
+ * Bit board of one shard: R local rows, Wd = W/32 uint32 words per row, row
+ * pitch `pitch` words.  Input row y of the shard (-k <= y < R + k) is read
+ * from: top + (y + k)*pitch for y < 0, mid + y*pitch for 0 <= y < R,
+ * bot + (y - R)*pitch for y >= R.  (One GPU: top = mid + (R-k)*pitch,
+ * bot = mid, the torus wrap; several GPUs: the k-row halo buffers received
+ * from the neighbouring ranks.)  Writes rows [row0, row0 + rows) of dst
+ * after k turns.  If count_slots is non-NULL the alive cells of the written
+ * rows are added to count_slots[0 .. GOL_COUNT_SLOTS*8) (sum them all). */
+#define GOL_COUNT_SLOTS 256
+int gol_dev_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
+                      int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int32_t k,
+                      int32_t cells_per_lane, int32_t strip_rows, uint64_t *count_slots,
+                      void *stream);
+/* Fill rows [0, rows) of a bit board with the synthetic board rows
+ * [grow0, grow0 + rows) of a W-wide torus (W % 64 == 0). */
+int gol_dev_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch,
+                        uint64_t seed, void *stream);
+/* Add popcount(rows x Wd words) to slots (GOL_COUNT_SLOTS*8 uint64). */
+int gol_dev_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch,
+                     uint64_t *slots, void *stream);
+/* Add the board-hash contribution of rows whose first global row is grow0. */
+int gol_dev_hash(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Wd, int64_t pitch,
+                 uint64_t *slots, void *stream);
+/* Bytes <-> bits for rows x W cells; pack also ORs 1 into *nonbinary when a
+ * byte other than 0/255 is seen (may be NULL). */
+int gol_dev_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits,
+                 int64_t pitch, uint32_t *nonbinary, void *stream);
+int gol_dev_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes,
+                   int64_t stride, void *stream);
+/* One exact-semantics byte turn (worker.go:15-70) for rows [y0, y1) of an
+ * H x W byte torus; out row i = next state of row y0 + i. */
+int gol_dev_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0,
+                       int64_t y1, uint8_t *out, int64_t out_stride, void *stream);
+
+/* ---------------------------------------------------------------- RPC service mirror
+ * The broker's net/rpc service `Operations` (broker.go:62-277) and the
+ * worker's `GameOfLifeOperations` (worker.go:77-86) with the gob field names
+ * of stubs.go:13-38.  A Go drop-in registers these names and forwards here. */
+typedef struct gol_request {     /* stubs.Request, stubs.go:20-29 */
+    const uint8_t *World;        /* ImageHeight x ImageWidth bytes, row pitch world_stride */
+    int64_t world_stride;
+    int64_t Turns;
+    int64_t ImageHeight;
+    int64_t ImageWidth;
+    int64_t Threads;
+    int64_t EndY;
+    int64_t StartY;
+    int64_t Worker;
+} gol_request;
+
+typedef struct gol_response {    /* stubs.Response, stubs.go:31-38 */
+    int32_t *Alive;              /* caller buffer for (X, Y) pairs (util.Cell, util/cell.go:4-5) */
+    int64_t alive_cap;           /* capacity in pairs */
+    int64_t alive_len;           /* out: len(Alive) (may exceed alive_cap: then truncated) */
+    int64_t AliveCount;          /* out */
+    int64_t TurnsCompleted;      /* out */
+    uint8_t *World;              /* caller buffer, ImageHeight x ImageWidth, pitch world_stride */
+    int64_t world_stride;
+    uint8_t *WorkSlice;          /* caller buffer, (EndY-StartY) x width, pitch work_stride */
+    int64_t work_stride;
+    int64_t Worker;
+} gol_response;
+
+typedef struct gol_broker gol_broker;
+int gol_broker_create(const gol_config *cfg, gol_broker **out);
+void gol_broker_destroy(gol_broker *b);
+int gol_broker_run(gol_broker *b, const gol_request *req, gol_response *res);      /* Operations.Run, broker.go:62-234 */
+int gol_broker_retrieve(gol_broker *b, const gol_request *req, gol_response *res); /* Operations.RetrieveCurrentData, broker.go:256-277 */
+int gol_broker_pause(gol_broker *b);                                              /* Operations.Pause, broker.go:251-254 */
+int gol_broker_quit(gol_broker *b);                                               /* Operations.Quit, broker.go:236-239 */
+int gol_broker_superquit(gol_broker *b);                                          /* Operations.SuperQuit, broker.go:241-249 */
+int gol_broker_paused(gol_broker *b, int32_t *paused);
+int gol_worker_update(const gol_request *req, gol_response *res);                 /* GameOfLifeOperations.Update, worker.go:77-80 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOLHIP_H */

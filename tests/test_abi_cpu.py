@@ -1,0 +1,119 @@
+"""CPU-side checks of the drop-in boundary (no GPU needed):
+
+* libgolhip.so loads and exports every symbol include/golhip.h declares, and the
+  ctypes table binds each of them;
+* the header is valid C and C++;
+* host logic that runs without a device: the partition (broker.go:135-206),
+  error codes instead of crashes, PGM codec, wire names of stubs.go.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "golhip.h")
+
+
+@pytest.fixture(scope="module")
+def G():
+    import golhip
+    golhip.lib()
+    return golhip
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gol_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol(G):
+    import ctypes
+    lib = ctypes.CDLL(G._lib.LIB_PATH)
+    decl = declared_functions()
+    assert len(decl) >= 30
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert sorted(n for n, _, _ in G._lib.SIGNATURES) == decl
+
+
+def test_nm_exports_match_header(G):
+    out = subprocess.run(["nm", "-D", "--defined-only", G._lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = sorted({l.split()[-1] for l in out.splitlines() if l.split()[-1].startswith("gol_")})
+    assert exported == declared_functions()
+
+
+@pytest.mark.parametrize("compiler,lang", [("gcc", "c"), ("g++", "c++")])
+def test_header_compiles(tmp_path, compiler, lang):
+    src = tmp_path / ("t.c" if lang == "c" else "t.cpp")
+    src.write_text('#include "golhip.h"\nint main(void){ return gol_abi_version() == GOL_ABI_VERSION ? 0 : 1; }\n')
+    subprocess.run([compiler, "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.dirname(HEADER), str(src)],
+                   check=True)
+
+
+def test_abi_version(G):
+    assert G.lib().gol_abi_version() == 1
+
+
+@pytest.mark.parametrize("H,T", [(512, 4), (512, 16), (16, 3), (64, 7), (17, 5), (10, 16), (1, 1), (0, 3)])
+def test_partition_matches_broker_formula(G, H, T):
+    for i in range(T):
+        assert G.partition_rows(H, T, i) == O.partition(H, T, i)
+
+
+def test_partition_errors(G):
+    for args in [(16, 0, 0), (16, 4, 4), (16, 4, -1), (-1, 2, 0)]:
+        with pytest.raises(G.GolError) as ei:
+            G.partition_rows(*args)
+        assert ei.value.code == G._lib.GOL_EINVAL
+
+
+def test_no_gpu_calls_fail_cleanly(G):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("has a GPU")
+    with pytest.raises(G.GolError):
+        G.Engine(16, 16)
+    with pytest.raises(G.GolError):
+        G.next_state_slab(np.zeros((16, 16), np.uint8), 0, 16)
+    with pytest.raises(G.GolError):
+        G.next_state_slab(np.zeros((16, 16), np.uint8), 5, 2)  # bad bounds: EINVAL before any HIP call
+
+
+def test_pgm_reader_matches_oracle_and_errors(G, golden_dir, tmp_path):
+    for name in os.listdir(os.path.join(golden_dir, "check", "images")):
+        p = os.path.join(golden_dir, "check", "images", name)
+        assert np.array_equal(G.read_pgm(p), O.read_pgm(p)[2])
+        assert G.write_pgm_bytes(G.read_pgm(p)) == open(p, "rb").read()
+    bad = tmp_path / "bad.pgm"
+    bad.write_bytes(b"P2\n2 2\n255\n\x00\x00\x00\x00")
+    with pytest.raises(G.GolError, match="Not a pgm file"):
+        G.read_pgm(str(bad))
+    bad.write_bytes(b"P5\n2 2\n15\n\x00\x00\x00\x00")
+    with pytest.raises(G.GolError, match="Incorrect maxval"):
+        G.read_pgm(str(bad))
+    p = os.path.join(golden_dir, "images", "16x16.pgm")
+    with pytest.raises(G.GolError, match="Incorrect width"):
+        G.read_pgm(p, width=17)
+
+
+def test_stub_names_match_reference(G):
+    """stubs.go:5-11 method names (the net/rpc ABI a Go drop-in keeps)."""
+    s = G.stubs if hasattr(G, "stubs") else __import__("golhip.stubs", fromlist=["x"])
+    assert s.GameOfLifeUpdate == "GameOfLifeOperations.Update"
+    assert s.BrokeOps == "Operations.Run"
+    assert s.Retrieve == "Operations.RetrieveCurrentData"
+    assert s.Pause == "Operations.Pause" and s.Quit == "Operations.Quit"
+    assert s.SuperQuit == "Operations.SuperQuit" and s.WorkerQuit == "GameOfLifeOperations.WorkerQuit"
+    req = s.Request()
+    for f in ["World", "Turns", "ImageHeight", "ImageWidth", "Threads", "EndY", "StartY", "Worker"]:
+        assert hasattr(req, f)
+    res = s.Response()
+    for f in ["Alive", "AliveCount", "TurnsCompleted", "World", "WorkSlice", "Worker"]:
+        assert hasattr(res, f)

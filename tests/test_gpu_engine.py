@@ -1,0 +1,280 @@
+"""GPU parity tests: libgolhip.so (gfx950 kernels) against the oracle and the
+reference's golden fixtures.  Every call goes through the C ABI.
+
+Mirrors the reference's end-to-end tests:
+  TestGol   gol_test.go:15-47     -> test_gol_matrix (sizes x turns x threads 1..16)
+  TestPgm   pgm_test.go:10-42     -> test_pgm_output
+  TestAlive count_test.go:17-69   -> test_alive_counts_csv / test_alive_parity_rule
+plus size-independent properties at the bench's full size.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [16, 64, 512]
+TURNS = [0, 1, 100]
+
+
+@pytest.fixture(scope="module")
+def golhip():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import golhip as G
+    G.lib()
+    return G
+
+
+def _golden_board(golden_dir, size):
+    return O.read_pgm(os.path.join(golden_dir, "images", f"{size}x{size}.pgm"), size, size)[2]
+
+
+def _golden_alive(golden_dir, size, turns):
+    """gol_test.go:88-129 readAliveCells: every nonzero byte of the golden PGM is alive."""
+    _, _, g = O.read_pgm(os.path.join(golden_dir, "check", "images", f"{size}x{size}x{turns}.pgm"))
+    ys, xs = np.nonzero(g)
+    return set(zip(xs.tolist(), ys.tolist())), g
+
+
+# ------------------------------------------------------------------ reference test matrix
+@pytest.mark.parametrize("size", SIZES)
+@pytest.mark.parametrize("turns", TURNS)
+def test_gol_matrix(golhip, golden_dir, size, turns):
+    """TestGol: Operations.Run's FinalTurnComplete alive list for 1..16 threads."""
+    board = _golden_board(golden_dir, size)
+    expected, gold = _golden_alive(golden_dir, size, turns)
+    ops = golhip.Operations(device=0)
+    for threads in range(1, 17):
+        res = ops.Run(golhip.Request(World=board, Turns=turns, ImageHeight=size, ImageWidth=size,
+                                     Threads=threads))
+        assert res.TurnsCompleted == turns
+        cells = [(c.X, c.Y) for c in res.Alive]
+        assert set(cells) == expected, f"{size}x{size}x{turns}-{threads}"
+        assert cells == sorted(cells, key=lambda c: (c[1], c[0]))  # row-major, broker.go:50-55
+        assert np.array_equal(res.World, gold)
+
+
+@pytest.mark.parametrize("size", SIZES)
+@pytest.mark.parametrize("turns", TURNS)
+def test_pgm_output(golhip, golden_dir, tmp_path, size, turns):
+    """TestPgm: the P5 file written from the device is byte-identical to check/images."""
+    with golhip.Engine(size, size, device=0) as e:
+        e.load_bytes(_golden_board(golden_dir, size))
+        e.step(turns)
+        out = tmp_path / f"{size}x{size}x{turns}.pgm"
+        e.write_pgm(str(out))
+    with open(os.path.join(golden_dir, "check", "images", f"{size}x{size}x{turns}.pgm"), "rb") as f:
+        assert out.read_bytes() == f.read()
+
+
+@pytest.mark.parametrize("size", SIZES)
+def test_alive_counts_csv(golhip, golden_dir, size):
+    """TestAlive: alive count after every turn 1..10000 equals check/alive/<s>x<s>.csv."""
+    expected = O.read_alive_csv(os.path.join(golden_dir, "check", "alive", f"{size}x{size}.csv"))
+    with golhip.Engine(size, size, device=0) as e:
+        e.load_bytes(_golden_board(golden_dir, size))
+        for t in range(1, 10001):
+            e.step(1)
+            assert e.alive_count() == expected[t], f"turn {t}"
+
+
+def test_alive_counts_chunked(golhip, golden_dir):
+    """The same counts when stepping in k-turn launches of mixed sizes (temporal blocking)."""
+    expected = O.read_alive_csv(os.path.join(golden_dir, "check", "alive", "512x512.csv"))
+    with golhip.Engine(512, 512, device=0, turns_per_launch=16) as e:
+        e.load_bytes(_golden_board(golden_dir, 512))
+        t = 0
+        for chunk in [1, 2, 3, 5, 8, 13, 16, 16, 31, 100, 250, 555] * 6:
+            e.step(chunk)
+            t += chunk
+            assert e.alive_count() == expected[t], f"turn {t}"
+
+
+def test_alive_parity_rule(golhip, golden_dir):
+    """count_test.go:47-51: after 10000 turns 512x512 alternates 5565 (even) / 5567 (odd)."""
+    with golhip.Engine(512, 512, device=0) as e:
+        e.load_bytes(_golden_board(golden_dir, 512))
+        e.step(10000)
+        for t in range(10001, 10011):
+            e.step(1)
+            assert e.alive_count() == (5565 if t % 2 == 0 else 5567)
+
+
+# ------------------------------------------------------------------ kernels vs oracle
+@pytest.mark.parametrize("shape", [(64, 64), (128, 256), (100, 192), (37, 320), (1, 64), (2, 128), (3, 64),
+                                   (256, 64 * 65), (16, 16), (48, 80), (20, 100), (7, 33)])
+@pytest.mark.parametrize("turns", [1, 2, 7, 33])
+def test_random_boards_vs_oracle(golhip, shape, turns):
+    H, W = shape
+    rng = np.random.default_rng(H * 1000 + W + turns)
+    board = (rng.random((H, W)) < 0.35).astype(np.uint8) * 255
+    ref = O.run(board, turns) if H * W * turns < 2_000_000 else O.unpack(O.bits_run(O.pack(board), turns))
+    with golhip.Engine(H, W, device=0) as e:
+        e.load_bytes(board)
+        e.step(turns)
+        assert np.array_equal(e.store_bytes(), ref)
+        assert e.alive_count() == int(np.count_nonzero(ref))
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("cpl", [32, 64, 128])
+def test_kernel_variants_vs_bit_oracle(golhip, k, cpl):
+    """Every (turns per launch, cells per lane) instantiation on a random torus."""
+    if k == 16 and cpl == 128:
+        pytest.skip("k=16 is built for 32/64 cells per lane only")
+    H, W = 300, 64 * 70
+    words = O.random_words(11 + k, 0, H, W // 64)
+    ref = O.bits_run(words, 45)
+    with golhip.Engine(H, W, device=0, turns_per_launch=k, cells_per_lane=cpl) as e:
+        e.load_random(11 + k)
+        assert e.hash() == O.hash_words(words)
+        e.step(45)
+        assert e.hash() == O.hash_words(ref)
+        assert np.array_equal(e.store_bytes(), O.unpack(ref))
+
+
+@pytest.mark.parametrize("strip", [1, 5, 32, 97])
+def test_strip_sizes(golhip, strip):
+    H, W = 211, 64 * 9
+    words = O.random_words(5, 0, H, W // 64)
+    ref = O.bits_run(words, 20)
+    with golhip.Engine(H, W, device=0, turns_per_launch=4, strip_rows=strip) as e:
+        e.load_random(5)
+        e.step(20)
+        assert e.hash() == O.hash_words(ref)
+
+
+def test_non_binary_bytes_first_turn(golhip):
+    """worker.go:26-37: only exactly-0 cells are born, only exactly-255 cells count/survive;
+    other bytes become 0.  Before turn 1 the loaded bytes are returned unchanged and count
+    as alive in the list (broker.go:52 uses != 0)."""
+    rng = np.random.default_rng(3)
+    for H, W in [(64, 128), (33, 48)]:
+        board = rng.choice(np.array([0, 255, 1, 7, 128, 254], dtype=np.uint8), size=(H, W),
+                           p=[.45, .4, .05, .04, .03, .03])
+        with golhip.Engine(H, W, device=0) as e:
+            e.load_bytes(board)
+            assert np.array_equal(e.store_bytes(), board)
+            assert e.alive_count() == int(np.count_nonzero(board))
+            cells = e.alive_cells()
+            assert [tuple(c) for c in cells.tolist()] == O.alive_cells(board)
+            e.step(1)
+            ref1 = O.run(board, 1)
+            assert np.array_equal(e.store_bytes(), ref1)
+            e.step(9)
+            assert np.array_equal(e.store_bytes(), O.run(board, 10))
+
+
+def test_next_state_slab_vs_oracle(golhip, golden_dir):
+    """GameOfLifeOperations.Update over every slab of the broker's partition."""
+    board = _golden_board(golden_dir, 512)
+    worker = golhip.GameOfLifeOperations()
+    for threads in (1, 3, 4, 7, 16):
+        slabs = []
+        for i in range(threads):
+            y0, y1 = golhip.partition_rows(512, threads, i)
+            assert (y0, y1) == O.partition(512, threads, i)
+            res = worker.Update(golhip.Request(World=board, StartY=y0, EndY=y1, Worker=i))
+            assert np.array_equal(res.WorkSlice, O.next_state_slab(board, y0, y1))
+            slabs.append(res.WorkSlice)
+        assert np.array_equal(np.concatenate(slabs), O.run(board, 1))
+    rng = np.random.default_rng(9)
+    odd = rng.choice(np.array([0, 255, 3], dtype=np.uint8), size=(50, 70))
+    assert np.array_equal(golhip.next_state_slab(odd, 13, 41), O.next_state_slab(odd, 13, 41))
+
+
+def test_alive_cells_row_major(golhip):
+    rng = np.random.default_rng(4)
+    board = (rng.random((130, 64 * 5)) < 0.2).astype(np.uint8) * 255
+    with golhip.Engine(130, 320, device=0) as e:
+        e.load_bytes(board)
+        e.step(3)
+        ref = O.run(board, 3)
+        got = [tuple(c) for c in e.alive_cells().tolist()]
+        assert got == O.alive_cells(ref)
+        part = e.alive_cells(cap=17)
+        assert [tuple(c) for c in part.tolist()] == O.alive_cells(ref)[:17]
+
+
+def test_empty_and_full_boards(golhip):
+    for fill, turns, expect in [(0, 5, 0), (255, 1, 0)]:
+        board = np.full((64, 128), fill, dtype=np.uint8)
+        with golhip.Engine(64, 128, device=0) as e:
+            e.load_bytes(board)
+            e.step(turns)
+            assert e.alive_count() == expect
+            assert len(e.alive_cells()) == expect
+
+
+def test_glider_translation(golhip):
+    """A glider moves (1,1) every 4 turns; on a torus it comes back after 4*H turns."""
+    H = W = 64
+    board = np.zeros((H, W), dtype=np.uint8)
+    for x, y in [(1, 0), (2, 1), (0, 2), (1, 2), (2, 2)]:
+        board[y, x] = 255
+    with golhip.Engine(H, W, device=0) as e:
+        e.load_bytes(board)
+        e.step(4)
+        assert np.array_equal(e.store_bytes(), np.roll(np.roll(board, 1, 0), 1, 1))
+        e.step(4 * H - 4)
+        assert np.array_equal(e.store_bytes(), board)
+
+
+def test_errors_are_codes_not_crashes(golhip):
+    with pytest.raises(golhip.GolError):
+        golhip.Engine(0, 64)
+    with golhip.Engine(32, 64, device=0) as e:
+        with pytest.raises(golhip.GolError):
+            e.step(-1)
+    with golhip.Engine(32, 48, device=0) as e:
+        with pytest.raises(golhip.GolError):
+            e.load_random(1)  # needs W % 64 == 0
+    ops = golhip.Operations(device=0)
+    with pytest.raises(golhip.GolError):
+        ops.RetrieveCurrentData(golhip.Request(ImageHeight=16, ImageWidth=16))  # no Run yet
+    with pytest.raises(golhip.GolError):
+        ops.Run(golhip.Request(World=np.zeros((16, 16), np.uint8), Turns=1, ImageHeight=16, ImageWidth=16,
+                               Threads=0))
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_tiled_board_matches_small_torus(golhip):
+    """A torus tiled with copies of a small torus evolves as the small one (every tile equal to
+    the oracle's small-board result) -- checks the kernel at a size the oracle cannot run."""
+    th, tw, reps_y, reps_x, turns = 256, 512, 64, 128, 40
+    rng = np.random.default_rng(21)
+    tile = (rng.random((th, tw)) < 0.4).astype(np.uint8) * 255
+    ref = O.unpack(O.bits_run(O.pack(tile), turns))
+    big = np.tile(tile, (reps_y, reps_x))  # 16384 x 65536
+    with golhip.Engine(th * reps_y, tw * reps_x, device=0) as e:
+        e.load_bytes(big)
+        del big
+        e.step(turns)
+        got = e.store_bytes().reshape(reps_y, th, reps_x, tw)
+        assert (got == ref[None, :, None, :]).all()
+        assert e.alive_count() == reps_y * reps_x * int(np.count_nonzero(ref))
+
+
+def test_bench_size_k_and_shard_invariance(golhip):
+    """2^17 x 2^20 (the bench's per-GPU torus): k=1, k=8 and k=16 launches give the same board
+    hash, and the fused popcount equals the popcount kernel."""
+    import torch
+    from golhip.sharded import ShardedBoard
+    H, W, turns = 1 << 17, 1 << 20, 16
+    hashes = []
+    for k in (1, 8, 16):
+        b = ShardedBoard(H, W, turns_per_launch=k)
+        b.load_random(1)
+        b.step(turns, count=True)
+        torch.cuda.synchronize()
+        fused = b.fused_count()
+        assert fused == b.alive_count()
+        hashes.append(b.hash())
+        del b
+        torch.cuda.empty_cache()
+    assert len(set(hashes)) == 1
