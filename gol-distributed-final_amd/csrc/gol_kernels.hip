@@ -169,10 +169,20 @@ struct BitsArgs {
     uint64_t *slots;
 };
 
+// Minimum waves per SIMD the register allocator must allow (occupancy floor).
+#ifndef GOL_WPE
+#define GOL_WPE(K, DW) 1
+#endif
+// Keep the scheduler from interleaving consecutive rows' pipelines (which
+// multiplies the live state); set to empty to let it.
+#ifndef GOL_SCHED_FENCE
+#define GOL_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 // grid.x: groups of 4 waves along the row; grid.y: strips of output rows.
 // Wave = one column group of 62*DW output words (+1 halo lane each side).
 template <int K, int DW>
-__global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_WPE(K, DW), 8))) bits_step_kernel(BitsArgs a)
 {
     const int lane = threadIdx.x & 63;
     const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -236,7 +246,9 @@ __global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
             }                                                                              \
         }
         GOL_STEP(0)
+        GOL_SCHED_FENCE();
         GOL_STEP(1)
+        GOL_SCHED_FENCE();
         GOL_STEP(2)
 #undef GOL_STEP
 #pragma unroll
