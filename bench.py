@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="weak", choices=["weak", "bit64k", "byte16k"])
-    ap.add_argument("--k", type=int, default=8, help="turns per launch (temporal blocking)")
+    ap.add_argument("--k", type=int, default=16, help="turns per launch (temporal blocking)")
     ap.add_argument("--cpl", type=int, default=0, help="cells per lane (32/64/128; 0 = library default)")
     ap.add_argument("--strip", type=int, default=0, help="rows per wave strip (0 = auto)")
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)

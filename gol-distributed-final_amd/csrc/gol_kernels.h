@@ -7,6 +7,10 @@
 #define GOL_COUNT_SLOTS 256
 #endif
 
+#ifndef GOL_DEFAULT_ALGO
+#define GOL_DEFAULT_ALGO 0
+#endif
+int golk_bits_algo();
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k);
 hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
                           int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw,

@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include "gol_kernels.h"
 
 namespace golk {
@@ -161,6 +163,83 @@ __device__ __forceinline__ void pipe_step(Pipe<K, DW> &p, const uint32_t (&in)[D
     for (int j = 0; j < DW; ++j) out[j] = cur[j];
 }
 
+// Vertical-first variant: the stage keeps the raw cells of the last rows (3 per
+// stage in the period-3 ring instead of 9 for horizontal sums), forms the
+// vertical 3-sum of each column, then sums three horizontally shifted 2-bit
+// column sums.  ~2 more VALU ops per word and stage, a third of the registers.
+template <int K, int DW>
+struct VPipe {
+    uint32_t c[K][3][DW];
+};
+
+template <int K, int DW, int S>
+__device__ __forceinline__ void vpipe_step(VPipe<K, DW> &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+{
+    constexpr int SA = (S + 1) % 3;
+    constexpr int SM = (S + 2) % 3;
+    uint32_t cur[DW];
+#pragma unroll
+    for (int j = 0; j < DW; ++j) cur[j] = in[j];
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+        uint32_t v0[DW], v1[DW];
+#pragma unroll
+        for (int j = 0; j < DW; ++j) {
+            p.c[g][S][j] = cur[j];
+            v0[j] = bitop3<TT_XOR3>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
+            v1[j] = bitop3<TT_MAJ>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
+        }
+        const uint32_t l0 = from_lower_lane(v0[DW - 1]), r0 = from_upper_lane(v0[0]);
+        const uint32_t l1 = from_lower_lane(v1[DW - 1]), r1 = from_upper_lane(v1[0]);
+#pragma unroll
+        for (int j = 0; j < DW; ++j) {
+            const uint32_t L0 = __builtin_amdgcn_alignbit(v0[j], j == 0 ? l0 : v0[j - 1], 31);
+            const uint32_t L1 = __builtin_amdgcn_alignbit(v1[j], j == 0 ? l1 : v1[j - 1], 31);
+            const uint32_t R0 = __builtin_amdgcn_alignbit(j == DW - 1 ? r0 : v0[j + 1], v0[j], 1);
+            const uint32_t R1 = __builtin_amdgcn_alignbit(j == DW - 1 ? r1 : v1[j + 1], v1[j], 1);
+            cur[j] = rule(L0, L1, v0[j], v1[j], R0, R1, p.c[g][SM][j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < DW; ++j) out[j] = cur[j];
+}
+
+template <int K, int DW, int ALGO> struct PipeSel;
+template <int K, int DW> struct PipeSel<K, DW, 0> {
+    typedef Pipe<K, DW> type;
+    static __device__ __forceinline__ void init(type &p)
+    {
+#pragma unroll
+        for (int g = 0; g < K; ++g)
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+#pragma unroll
+                for (int j = 0; j < DW; ++j) { p.h0[g][s][j] = 0; p.h1[g][s][j] = 0; p.cc[g][s][j] = 0; }
+    }
+    template <int S>
+    static __device__ __forceinline__ void step(type &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+    {
+        pipe_step<K, DW, S>(p, in, out);
+    }
+};
+template <int K, int DW> struct PipeSel<K, DW, 1> {
+    typedef VPipe<K, DW> type;
+    static __device__ __forceinline__ void init(type &p)
+    {
+#pragma unroll
+        for (int g = 0; g < K; ++g)
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+#pragma unroll
+                for (int j = 0; j < DW; ++j) p.c[g][s][j] = 0;
+    }
+    template <int S>
+    static __device__ __forceinline__ void step(type &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+    {
+        vpipe_step<K, DW, S>(p, in, out);
+    }
+};
+
 struct BitsArgs {
     const uint32_t *top, *mid, *bot;
     uint32_t *dst;
@@ -169,20 +248,11 @@ struct BitsArgs {
     uint64_t *slots;
 };
 
-// Minimum waves per SIMD the register allocator must allow (occupancy floor).
-#ifndef GOL_WPE
-#define GOL_WPE(K, DW) 1
-#endif
-// Keep the scheduler from interleaving consecutive rows' pipelines (which
-// multiplies the live state); set to empty to let it.
-#ifndef GOL_SCHED_FENCE
-#define GOL_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
 
 // grid.x: groups of 4 waves along the row; grid.y: strips of output rows.
 // Wave = one column group of 62*DW output words (+1 halo lane each side).
-template <int K, int DW>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_WPE(K, DW), 8))) bits_step_kernel(BitsArgs a)
+template <int K, int DW, int ALGO>
+__global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
 {
     const int lane = threadIdx.x & 63;
     const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -211,13 +281,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_WP
         return base + y * a.pitch + lane_off;
     };
 
-    Pipe<K, DW> p;
-#pragma unroll
-    for (int g = 0; g < K; ++g)
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-#pragma unroll
-            for (int j = 0; j < DW; ++j) { p.h0[g][s][j] = 0; p.h1[g][s][j] = 0; p.cc[g][s][j] = 0; }
+    typedef PipeSel<K, DW, ALGO> PS;
+    typename PS::type p;
+    PS::init(p);
 
     uint32_t buf[3][DW];
 #pragma unroll
@@ -233,7 +299,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_WP
         uint32_t out[DW];
 #define GOL_STEP(S)                                                                        \
         {                                                                                  \
-            pipe_step<K, DW, S>(p, buf[S], out);                                           \
+            PS::template step<S>(p, buf[S], out);                                           \
             const int64_t t = t0 + S;                                                      \
             const int64_t y = s0 + t - 2 * K; /* row emitted by the last stage */          \
             if (t >= 2 * K && y < s1) {                                                    \
@@ -246,9 +312,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_WP
             }                                                                              \
         }
         GOL_STEP(0)
-        GOL_SCHED_FENCE();
         GOL_STEP(1)
-        GOL_SCHED_FENCE();
         GOL_STEP(2)
 #undef GOL_STEP
 #pragma unroll
@@ -559,27 +623,38 @@ static inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 16)
     return (int)g;
 }
 
-template <int K, int DW>
+template <int K, int DW, int ALGO>
 static hipError_t launch_bits(const BitsArgs &a, hipStream_t s)
 {
     const int nstrips = (int)((a.rows + a.strip - 1) / a.strip);
     dim3 grid((a.ngroups + 3) / 4, nstrips);
-    hipLaunchKernelGGL((bits_step_kernel<K, DW>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((bits_step_kernel<K, DW, ALGO>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-template <int DW>
+template <int DW, int ALGO>
 static hipError_t launch_bits_k(int k, const BitsArgs &a, hipStream_t s)
 {
     switch (k) {
-    case 1: return launch_bits<1, DW>(a, s);
-    case 2: return launch_bits<2, DW>(a, s);
-    case 4: return launch_bits<4, DW>(a, s);
-    case 8: return launch_bits<8, DW>(a, s);
-    case 16: if constexpr (DW <= 2) return launch_bits<16, DW>(a, s);
+    case 1: return launch_bits<1, DW, ALGO>(a, s);
+    case 2: return launch_bits<2, DW, ALGO>(a, s);
+    case 4: return launch_bits<4, DW, ALGO>(a, s);
+    case 8: return launch_bits<8, DW, ALGO>(a, s);
+    case 16: if constexpr (DW <= 2) return launch_bits<16, DW, ALGO>(a, s);
              return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
     }
+}
+
+// Step formulation: 0 = horizontal sums first, 1 = vertical sums first.
+// GOL_BITS_ALGO overrides the default (used by tools/sweep.py).
+int golk_bits_algo()
+{
+    static int algo = [] {
+        const char *e = getenv("GOL_BITS_ALGO");
+        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : GOL_DEFAULT_ALGO;
+    }();
+    return algo;
 }
 
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
@@ -606,10 +681,14 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.strip = strip > 0 ? strip : golk_auto_strip(rows, a.ngroups, k);
     a.slots = slots;
     if (rows <= 0) return hipSuccess;
-    switch (dw) {
-    case 1: return launch_bits_k<1>(k, a, s);
-    case 2: return launch_bits_k<2>(k, a, s);
-    case 4: return launch_bits_k<4>(k, a, s);
+    const int algo = golk_bits_algo();
+    switch (dw * 2 + algo) {
+    case 2: return launch_bits_k<1, 0>(k, a, s);
+    case 3: return launch_bits_k<1, 1>(k, a, s);
+    case 4: return launch_bits_k<2, 0>(k, a, s);
+    case 5: return launch_bits_k<2, 1>(k, a, s);
+    case 8: return launch_bits_k<4, 0>(k, a, s);
+    case 9: return launch_bits_k<4, 1>(k, a, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgolhip.so")
+# GOLHIP_LIB selects an alternative build of the same library (kernel experiments in tools/).
+LIB_PATH = os.environ.get("GOLHIP_LIB") or os.path.join(_HERE, "libgolhip.so")
 
 GOL_OK = 0
 GOL_EINVAL = -1

@@ -134,6 +134,18 @@ class ShardedBoard:
         if self.nranks == 1:
             return None
         g = self.group
+        if self.device.type == "cuda" and dist.get_backend(g) == "gloo":
+            # gloo has no device P2P: stage the halo rows through host memory (used to test
+            # several ranks sharing one GPU; production runs use nccl = RCCL over xGMI).
+            up, down = cur[:k].cpu(), cur[self.R - k:].cpu()
+            bot, top = torch.empty_like(up), torch.empty_like(down)
+            ops = [dist.P2POp(dist.isend, up, self.prev, g), dist.P2POp(dist.irecv, bot, self.next, g),
+                   dist.P2POp(dist.isend, down, self.next, g), dist.P2POp(dist.irecv, top, self.prev, g)]
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+            self.ghost_bot[:k].copy_(bot)
+            self.ghost_top[:k].copy_(top)
+            return []
         ops = [dist.P2POp(dist.isend, cur[:k], self.prev, g),
                dist.P2POp(dist.irecv, self.ghost_bot[:k], self.next, g),
                dist.P2POp(dist.isend, cur[self.R - k:], self.next, g),

@@ -1,0 +1,56 @@
+"""Summarise a tools/profile.sh run into profiles/<tag>/ (tracked):
+  kernel_stats.csv       rocprofv3 --stats summary of the bench command
+  pmc_summary.json       per-kernel means of the PMC passes + derived HBM bytes, clock, VALU use
+and update profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+
+HBM bytes per launch = FETCH_SIZE*2 + WRITE_SIZE (KiB -> bytes), the gfx950 correction of
+MI355X_MICROARCH.md §HBM (FETCH_SIZE reports half of a wide streaming read)."""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag, key = sys.argv[1], sys.argv[2]           # e.g. r01 weak:k16:cpl0
+src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+dst = os.path.join(ROOT, "profiles", tag)
+os.makedirs(dst, exist_ok=True)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+
+means = collections.defaultdict(dict)
+for d in sorted(os.listdir(src)):
+    f = os.path.join(src, d, "run_counter_collection.csv")
+    if not d.startswith("pmc_") or not os.path.exists(f):
+        continue
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        acc[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (k, c), v in acc.items():
+        means[k][c] = sum(v) / len(v)
+
+stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
+out = {}
+for k, c in means.items():
+    ns = float(stats[k]["AverageNs"]) if k in stats else None
+    e = {"counters": c, "avg_ns_trace": ns}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        b = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        e["hbm_bytes_per_launch"] = b
+        if ns:
+            e["hbm_GBs"] = b / ns
+    if "GRBM_GUI_ACTIVE" in c and ns:
+        e["clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / ns
+        if "SQ_INSTS_VALU" in c:
+            cyc = c["GRBM_GUI_ACTIVE"] / 8
+            e["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (256 * 4 * 0.5 * cyc)
+    out[k] = e
+json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+main = max(out, key=lambda k: out[k].get("avg_ns_trace") or 0)
+tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+t = json.load(open(tp)) if os.path.exists(tp) else {}
+if "hbm_bytes_per_launch" in out[main]:
+    t[key] = {"kernel": main, "bytes_per_launch": out[main]["hbm_bytes_per_launch"], "profile": f"profiles/{tag}"}
+    json.dump(t, open(tp, "w"), indent=1)
+print(json.dumps(out[main], indent=1))
