@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample length")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="testing only: every rank uses cuda:0 (multi-rank logic on a 1-GPU box, with --backend gloo)")
     return ap.parse_args()
 
 
@@ -57,9 +60,14 @@ def setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.share_gpu:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     return rank, world, local
 
 
@@ -123,12 +131,13 @@ def cpu_baseline(args, H, W, k):
                       f"the Go reference cannot be built here"}
 
 
-def load_pmc(workload, k, cpl):
+def load_pmc(key):
+    """Measured HBM bytes per launch for this exact configuration (tools/pmc_summary.py)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(f"{workload}:k{k}:cpl{cpl}")
+        return d.get(key)
     except (OSError, ValueError):
         return None
 
@@ -167,7 +176,7 @@ def run_bits(args, rank, world):
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     from golhip import lib
     info = {"turns_per_step": k, "cells_per_lane": args.cpl or 32, "strip_rows": args.strip or "auto"}
-    pmc = load_pmc(args.workload, k, args.cpl)
+    pmc = load_pmc(f"{args.workload}:{H}x{W}:n{world}:k{k}:cpl{args.cpl}")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc.get("bytes_per_launch") if pmc else None,
@@ -222,7 +231,7 @@ def run_bytes(args, rank, world):
     value = H * W * world * args.steps / dt
     kms = sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
     achieved = BYTES_BYTES_PER_UPDATE * H * W / (kms * 1e-3) / 1e9
-    pmc = load_pmc("byte16k", 1, 0)
+    pmc = load_pmc(f"byte16k:{H}x{W}:n1:k1:cpl0")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("bytes_per_launch") if pmc else None,
             "basis": f"{BYTES_BYTES_PER_UPDATE} B/cell-update x {H}x{W} cells / {kms:.3f} ms mean launch"}

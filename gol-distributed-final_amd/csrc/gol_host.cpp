@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -75,6 +76,22 @@ struct Operations {
     bool running = false;
     int pending_pause = 0, pending_quit = 0;
     bool paused = false, shut_down = false;
+    // Callers other than the turn loop announce themselves here before locking `mu`;
+    // the loop yields the lock between chunks while any are waiting, so queries and
+    // control calls are served within one chunk (std::mutex alone is not fair).
+    std::atomic<int> waiters{0};
+
+    struct Access {  // RAII: announce, lock, and on exit release + wake the turn loop
+        Operations &o;
+        std::unique_lock<std::mutex> lk;
+        explicit Access(Operations &op) : o(op), lk((op.waiters.fetch_add(1), op.mu)) {}
+        ~Access()
+        {
+            o.waiters.fetch_sub(1);
+            lk.unlock();
+            o.cv.notify_all();
+        }
+    };
 
     ~Operations()
     {
@@ -154,8 +171,8 @@ struct Operations {
             cTurn += n;  // the (turn, board) pair is updated atomically under mu
             if (ms < 5.0 && chunk < (1LL << 20)) chunk *= 2;
             else if (ms > 20.0 && chunk > 1) chunk /= 2;
-            lk.unlock();  // let Retrieve / Pause / Quit in
-            lk.lock();
+            // let Retrieve / Pause / Quit in before the next chunk
+            cv.wait(lk, [&] { return waiters.load() == 0; });
         }
         if (rc == GOL_OK) {
             res->TurnsCompleted = cTurn;  // broker.go:228-230
@@ -171,7 +188,7 @@ struct Operations {
     int RetrieveCurrentData(const stubs::Request &req, stubs::Response *res)
     {
         if (!res) return gol_set_error(GOL_EINVAL, "res is NULL");
-        std::unique_lock<std::mutex> lk(mu);
+        Access acc(*this);
         if (!have_world) return gol_set_error(GOL_ESTATE, "no board: Operations.Run has not been called");
         if ((req.ImageHeight && req.ImageHeight != H) || (req.ImageWidth && req.ImageWidth != W))
             return gol_set_error(GOL_EINVAL, "request size %lldx%lld does not match the board %lldx%lld",
@@ -198,7 +215,7 @@ struct Operations {
 
     int Pause()  // broker.go:251-254
     {
-        std::lock_guard<std::mutex> lk(mu);
+        Access acc(*this);
         if (shut_down) return gol_set_error(GOL_EQUIT, "broker has shut down");
         pending_pause++;
         cv.notify_all();
@@ -207,7 +224,7 @@ struct Operations {
 
     int Quit()  // broker.go:236-239
     {
-        std::lock_guard<std::mutex> lk(mu);
+        Access acc(*this);
         if (shut_down) return gol_set_error(GOL_EQUIT, "broker has shut down");
         pending_quit++;
         cv.notify_all();
@@ -216,7 +233,7 @@ struct Operations {
 
     int SuperQuit()  // broker.go:241-249: stop the loop, the workers and the listener
     {
-        std::lock_guard<std::mutex> lk(mu);
+        Access acc(*this);
         if (running) pending_quit++;
         shut_down = true;
         cv.notify_all();
@@ -305,7 +322,7 @@ extern "C" int gol_broker_superquit(gol_broker *b)
 extern "C" int gol_broker_paused(gol_broker *b, int32_t *paused)
 {
     if (!b || !paused) return gol_set_error(GOL_EINVAL, "NULL argument");
-    std::lock_guard<std::mutex> lk(b->ops.mu);
+    Operations::Access acc(b->ops);
     *paused = b->ops.paused ? 1 : 0;
     return GOL_OK;
 }

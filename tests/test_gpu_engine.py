@@ -278,3 +278,62 @@ def test_bench_size_k_and_shard_invariance(golhip):
         del b
         torch.cuda.empty_cache()
     assert len(set(hashes)) == 1
+
+
+# ------------------------------------------------------------------ broker control path
+def test_alive_events_during_run_pause_quit(golhip, golden_dir):
+    """count_test.go:17-69 (TestAlive) through the broker mirror: a 10^8-turn Run on 512x512
+    with 8 threads; RetrieveCurrentData (the 2-s ticker of distributor.go:39-51) must return
+    (turn, count) pairs that match check/alive (or the 5565/5567 parity rule past turn 10000);
+    Pause freezes the turn (broker.go:251-254), a second Pause resumes, Quit ends the Run with
+    the turns completed so far (broker.go:236-239)."""
+    import threading
+    import time
+    expected = O.read_alive_csv(os.path.join(golden_dir, "check", "alive", "512x512.csv"))
+    board = _golden_board(golden_dir, 512)
+    ops = golhip.Operations(device=0)
+    req = golhip.Request(World=board, Turns=10**8, ImageHeight=512, ImageWidth=512, Threads=8)
+    out = {}
+    th = threading.Thread(target=lambda: out.update(res=ops.Run(req)))
+    th.start()
+    try:
+        seen = []
+        deadline = time.time() + 60
+        while len(seen) < 5 and time.time() < deadline:
+            time.sleep(0.05)
+            r = ops.RetrieveCurrentData(golhip.Request(ImageHeight=512, ImageWidth=512), alive=False, world=False)
+            t, c = r.TurnsCompleted, r.AliveCount
+            if t == 0:
+                assert c == 0  # cWorld is all-zero before the first turn (broker.go:67-70)
+                continue
+            want = expected[t] if t <= 10000 else (5565 if t % 2 == 0 else 5567)
+            assert c == want, f"turn {t}: {c} != {want}"
+            seen.append(t)
+        assert len(seen) == 5 and seen == sorted(seen)
+        ops.Pause()
+        time.sleep(0.2)
+        assert ops.paused
+        t1 = ops.RetrieveCurrentData(golhip.Request(ImageHeight=512, ImageWidth=512), alive=False).TurnsCompleted
+        time.sleep(0.2)
+        r2 = ops.RetrieveCurrentData(golhip.Request(ImageHeight=512, ImageWidth=512))
+        assert r2.TurnsCompleted == t1  # paused: no progress
+        assert len(r2.Alive) == r2.AliveCount
+        ops.Pause()  # resume
+        time.sleep(0.2)
+        assert not ops.paused
+        assert ops.RetrieveCurrentData(golhip.Request(ImageHeight=512, ImageWidth=512),
+                                       alive=False, world=False).TurnsCompleted > t1
+    finally:
+        ops.Quit()
+        th.join(60)
+    assert not th.is_alive()
+    res = out["res"]
+    t = res.TurnsCompleted
+    assert 0 < t < 10**8
+    want = expected[t] if t <= 10000 else (5565 if t % 2 == 0 else 5567)
+    assert len(res.Alive) == want
+    ys, xs = np.nonzero(res.World)
+    assert [(c.X, c.Y) for c in res.Alive] == list(zip(xs.tolist(), ys.tolist()))
+    ops.SuperQuit()
+    with pytest.raises(golhip.GolError):
+        ops.Run(golhip.Request(World=board, Turns=1, ImageHeight=512, ImageWidth=512, Threads=1))

@@ -13,7 +13,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-tag, key = sys.argv[1], sys.argv[2]           # e.g. r01 weak:k16:cpl0
+tag, key = sys.argv[1], sys.argv[2]  # e.g. r01 weak:131072x1048576:n1:k16:cpl0 (bench.py load_pmc key)
 src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
 dst = os.path.join(ROOT, "profiles", tag)
 os.makedirs(dst, exist_ok=True)
