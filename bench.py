@@ -191,6 +191,9 @@ def run_bits(args, rank, world):
 
 
 def run_bytes(args, rank, world):
+    """Config 2: 16384 x 16384 byte-per-cell torus.  The board stays one byte per cell in HBM;
+    with --k > 1 each launch runs k turns (gol_dev_bytes_step_k: 0/255 bytes packed to bits in
+    registers), with --k 1 the exact one-turn byte kernel (gol_dev_bytes_step)."""
     from golhip._lib import check, lib
     from golhip.sharded import HipKernels
     H = W = 16384
@@ -203,6 +206,7 @@ def run_bytes(args, rank, world):
     b = torch.empty_like(a)
     del bits
     stream = torch.cuda.current_stream().cuda_stream
+    k = max(kk for kk in (16, 8, 4, 2, 1) if kk <= args.k)
     pairs = []
     cur = [a, b]
 
@@ -211,7 +215,11 @@ def run_bytes(args, rank, world):
         if timed:
             s = torch.cuda.Event(enable_timing=True)
             s.record()
-        check(lib().gol_dev_bytes_step(src.data_ptr(), H, W, W, 0, H, dst.data_ptr(), W, stream))
+        if k == 1:
+            check(lib().gol_dev_bytes_step(src.data_ptr(), H, W, W, 0, H, dst.data_ptr(), W, stream))
+        else:
+            check(lib().gol_dev_bytes_step_k(src[H - k:].data_ptr(), src.data_ptr(), src.data_ptr(), dst.data_ptr(),
+                                             H, W, W, 0, H, k, args.strip, None, stream))
         if timed:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
@@ -228,14 +236,16 @@ def run_bytes(args, rank, world):
     dt = time.perf_counter() - t0
     barrier(world)
     dt = max_over_ranks(dt, world)
-    value = H * W * world * args.steps / dt
+    value = H * W * world * k * args.steps / dt
     kms = sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
-    achieved = BYTES_BYTES_PER_UPDATE * H * W / (kms * 1e-3) / 1e9
-    pmc = load_pmc(f"byte16k:{H}x{W}:n1:k1:cpl0")
+    achieved = BYTES_BYTES_PER_UPDATE * H * W * k / (kms * 1e-3) / 1e9
+    pmc = load_pmc(f"byte16k:{H}x{W}:n1:k{k}:cpl0")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("bytes_per_launch") if pmc else None,
-            "basis": f"{BYTES_BYTES_PER_UPDATE} B/cell-update x {H}x{W} cells / {kms:.3f} ms mean launch"}
-    cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": 1,
+            "basis": f"{BYTES_BYTES_PER_UPDATE} B/cell-update x {H}x{W} cells x {k} turns per launch / "
+                     f"{kms:.3f} ms mean launch",
+            "hbm_min_bytes_frac": round(2 * H * W / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k,
            "parallelism": f"replicas{world}" if world > 1 else "1gpu"}
     return value, dt, cfg, roof, "u8 (byte per cell)"
 

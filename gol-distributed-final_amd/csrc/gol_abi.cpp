@@ -217,7 +217,12 @@ extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_
         HIPCHK(hipMemcpy2DAsync(e->bytes[0], e->bstride, world, stride, e->W, e->H, hipMemcpyHostToDevice,
                                 e->stream));
         e->bcur = 0;
+        HIPCHK(hipMemsetAsync(e->flag, 0, sizeof(uint32_t), e->stream));
+        HIPCHK(golk_nonbinary(e->bytes[0], e->H, e->W, e->bstride, e->flag, e->stream));
+        uint32_t nb = 0;
+        HIPCHK(hipMemcpyAsync(&nb, e->flag, sizeof nb, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
+        e->bytes_binary = nb == 0;
         return GOL_OK;
     }
     // pack row chunks into the bit board; remember whether any byte is neither 0 nor 255
@@ -240,6 +245,7 @@ extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_
                                 e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
         e->bcur = 0;
+        e->bytes_binary = false;
         e->bit_mode = false;
     } else {
         free_bytes(e);
@@ -266,6 +272,18 @@ extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
 int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots)
 {
     while (turns > 0) {
+        if (!e->bit_mode && e->bytes_binary && e->W % 32 == 0) {
+            // 0/255 byte board: k turns per launch on the bytes (torus wrap through top/bot)
+            const int k = pick_k(e->k, turns, e->H, 1);
+            const uint8_t *mid = e->bytes[e->bcur];
+            HIPCHK(golk_bytes_blocked(mid + (e->H - k) * e->bstride, mid, mid, e->bytes[1 - e->bcur], e->H, e->W,
+                                      e->bstride, 0, e->H, k, e->strip, turns == k ? count_slots : nullptr,
+                                      e->stream));
+            e->bcur = 1 - e->bcur;
+            e->turn += k;
+            turns -= k;
+            continue;
+        }
         if (!e->bit_mode) {
             const int nb = 1 - e->bcur;
             HIPCHK(golk_bytes_step(e->bytes[e->bcur], e->H, e->W, e->bstride, 0, e->H, e->bytes[nb], e->bstride,
@@ -273,6 +291,7 @@ int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots)
             e->bcur = nb;
             e->turn += 1;
             turns -= 1;
+            e->bytes_binary = true;  // one exact turn leaves only 0/255
             if (e->bit_capable) {
                 // board is now strictly 0/255: continue on the bit board
                 HIPCHK(golk_pack(e->bytes[e->bcur], e->H, e->W, e->bstride, e->bits[0], e->pitch, nullptr,
@@ -530,6 +549,19 @@ extern "C" int gol_dev_unpack(const uint32_t *bits, int64_t rows, int64_t W, int
     if (!bytes || !bits || rows < 0 || W <= 0 || W % 32 || stride < W || pitch < W / 32)
         return gol_set_error(GOL_EINVAL, "bad unpack arguments");
     LAUNCH(golk_unpack(bits, rows, W, pitch, bytes, stride, (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_bytes_step_k(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst,
+                                    int64_t R, int64_t W, int64_t stride, int64_t row0, int64_t rows, int32_t k,
+                                    int32_t strip_rows, uint64_t *count_slots, void *stream)
+{
+    if (!top || !mid || !bot || !dst || R <= 0 || W <= 0 || W % 32 || stride < W || stride % 16 || row0 < 0 ||
+        rows < 0 || row0 + rows > R || !(k == 1 || k == 2 || k == 4 || k == 8 || k == 16) || k > R ||
+        (((uintptr_t)mid | (uintptr_t)top | (uintptr_t)bot | (uintptr_t)dst) & 15))
+        return gol_set_error(GOL_EINVAL, "bad bytes_step_k arguments (R=%lld W=%lld stride=%lld k=%d)",
+                             (long long)R, (long long)W, (long long)stride, k);
+    LAUNCH(golk_bytes_blocked(top, mid, bot, dst, R, W, stride, row0, rows, k, strip_rows, count_slots,
+                              (hipStream_t)stream));
 }
 
 extern "C" int gol_dev_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0,

@@ -28,6 +28,7 @@ struct gol_engine {
     int cur = 0;
     uint8_t *bytes[2] = {nullptr, nullptr};
     int bcur = 0;
+    bool bytes_binary = false;  // byte board holds only 0/255 (k-turn byte kernel allowed)
     uint64_t *slots = nullptr;  // GOL_COUNT_SLOTS * 8 uint64 reduction slots
     uint32_t *flag = nullptr;
     uint8_t *staging = nullptr;       // device byte rows for chunked copies

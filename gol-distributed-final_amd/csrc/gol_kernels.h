@@ -17,6 +17,10 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
                           int strip, uint64_t *slots, hipStream_t s);
 hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0, int64_t y1,
                            uint8_t *out, int64_t out_stride, hipStream_t s);
+hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst, int64_t R,
+                              int64_t W, int64_t pitch, int64_t row0, int64_t rows, int k, int strip, uint64_t *slots,
+                              hipStream_t s);
+hipError_t golk_nonbinary(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *flag, hipStream_t s);
 hipError_t golk_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch, uint64_t seed,
                             hipStream_t s);
 hipError_t golk_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots,

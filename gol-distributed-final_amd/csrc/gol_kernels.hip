@@ -163,17 +163,29 @@ __device__ __forceinline__ void pipe_step(Pipe<K, DW> &p, const uint32_t (&in)[D
     for (int j = 0; j < DW; ++j) out[j] = cur[j];
 }
 
-// Vertical-first variant: the stage keeps the raw cells of the last rows (3 per
-// stage in the period-3 ring instead of 9 for horizontal sums), forms the
-// vertical 3-sum of each column, then sums three horizontally shifted 2-bit
-// column sums.  ~2 more VALU ops per word and stage, a third of the registers.
-template <int K, int DW>
-struct VPipe {
-    uint32_t c[K][3][DW];
-};
+// Shifted-frame variant: the horizontal 3-sum is formed from the cell and its
+// two LEFT neighbours, S'[p] = c[p] + c[p-1] + c[p-2] = the 3-sum centred on p-1,
+// so a stage needs one DPP (left word) instead of two and the centre cell is
+// c << 1.  Every generation moves the frame one bit to the left; after K
+// generations one funnel shift with the right neighbour word realigns the row.
+template <int DW>
+__device__ __forceinline__ void hsum_left(const uint32_t (&c)[DW], uint32_t (&h0)[DW], uint32_t (&h1)[DW],
+                                          uint32_t (&ctr)[DW])
+{
+    const uint32_t left_in = from_lower_lane(c[DW - 1]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+        const uint32_t wl = (j == 0) ? left_in : c[j - 1];
+        const uint32_t L1 = __builtin_amdgcn_alignbit(c[j], wl, 31);  // c[p-1] at bit p
+        const uint32_t L2 = __builtin_amdgcn_alignbit(c[j], wl, 30);  // c[p-2] at bit p
+        h0[j] = bitop3<TT_XOR3>(L1, c[j], L2);
+        h1[j] = bitop3<TT_MAJ>(L1, c[j], L2);
+        ctr[j] = L1;
+    }
+}
 
 template <int K, int DW, int S>
-__device__ __forceinline__ void vpipe_step(VPipe<K, DW> &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+__device__ __forceinline__ void spipe_step(Pipe<K, DW> &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
 {
     constexpr int SA = (S + 1) % 3;
     constexpr int SM = (S + 2) % 3;
@@ -182,26 +194,38 @@ __device__ __forceinline__ void vpipe_step(VPipe<K, DW> &p, const uint32_t (&in)
     for (int j = 0; j < DW; ++j) cur[j] = in[j];
 #pragma unroll
     for (int g = 0; g < K; ++g) {
-        uint32_t v0[DW], v1[DW];
+        hsum_left<DW>(cur, p.h0[g][S], p.h1[g][S], p.cc[g][S]);
 #pragma unroll
-        for (int j = 0; j < DW; ++j) {
-            p.c[g][S][j] = cur[j];
-            v0[j] = bitop3<TT_XOR3>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
-            v1[j] = bitop3<TT_MAJ>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
-        }
-        const uint32_t l0 = from_lower_lane(v0[DW - 1]), r0 = from_upper_lane(v0[0]);
-        const uint32_t l1 = from_lower_lane(v1[DW - 1]), r1 = from_upper_lane(v1[0]);
-#pragma unroll
-        for (int j = 0; j < DW; ++j) {
-            const uint32_t L0 = __builtin_amdgcn_alignbit(v0[j], j == 0 ? l0 : v0[j - 1], 31);
-            const uint32_t L1 = __builtin_amdgcn_alignbit(v1[j], j == 0 ? l1 : v1[j - 1], 31);
-            const uint32_t R0 = __builtin_amdgcn_alignbit(j == DW - 1 ? r0 : v0[j + 1], v0[j], 1);
-            const uint32_t R1 = __builtin_amdgcn_alignbit(j == DW - 1 ? r1 : v1[j + 1], v1[j], 1);
-            cur[j] = rule(L0, L1, v0[j], v1[j], R0, R1, p.c[g][SM][j]);
-        }
+        for (int j = 0; j < DW; ++j)
+            cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j],
+                          p.h0[g][S][j], p.h1[g][S][j], p.cc[g][SM][j]);
     }
 #pragma unroll
     for (int j = 0; j < DW; ++j) out[j] = cur[j];
+}
+
+// One pipeline stage (generation g+1) of one row step S, in place on `cur`.
+template <int K, int DW, int S>
+__device__ __forceinline__ void hstage(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
+{
+    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < DW; ++j) p.cc[g][S][j] = cur[j];
+    hsum<DW>(p.cc[g][S], p.h0[g][S], p.h1[g][S]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j)
+        cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j], p.h0[g][S][j],
+                      p.h1[g][S][j], p.cc[g][SM][j]);
+}
+template <int K, int DW, int S>
+__device__ __forceinline__ void sstage(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
+{
+    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
+    hsum_left<DW>(cur, p.h0[g][S], p.h1[g][S], p.cc[g][S]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j)
+        cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j], p.h0[g][S][j],
+                      p.h1[g][S][j], p.cc[g][SM][j]);
 }
 
 template <int K, int DW, int ALGO> struct PipeSel;
@@ -217,26 +241,17 @@ template <int K, int DW> struct PipeSel<K, DW, 0> {
                 for (int j = 0; j < DW; ++j) { p.h0[g][s][j] = 0; p.h1[g][s][j] = 0; p.cc[g][s][j] = 0; }
     }
     template <int S>
-    static __device__ __forceinline__ void step(type &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+    static __device__ __forceinline__ void stage(type &p, const int g, uint32_t (&cur)[DW])
     {
-        pipe_step<K, DW, S>(p, in, out);
+        hstage<K, DW, S>(p, g, cur);
     }
 };
-template <int K, int DW> struct PipeSel<K, DW, 1> {
-    typedef VPipe<K, DW> type;
-    static __device__ __forceinline__ void init(type &p)
-    {
-#pragma unroll
-        for (int g = 0; g < K; ++g)
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-#pragma unroll
-                for (int j = 0; j < DW; ++j) p.c[g][s][j] = 0;
-    }
+template <int K, int DW> struct PipeSel<K, DW, 1> : PipeSel<K, DW, 0> {
+    typedef Pipe<K, DW> type;
     template <int S>
-    static __device__ __forceinline__ void step(type &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+    static __device__ __forceinline__ void stage(type &p, const int g, uint32_t (&cur)[DW])
     {
-        vpipe_step<K, DW, S>(p, in, out);
+        sstage<K, DW, S>(p, g, cur);
     }
 };
 
@@ -296,29 +311,147 @@ __global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
 #pragma unroll
         for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + t0 + 3 + s), nxt[s]);
 
-        uint32_t out[DW];
-#define GOL_STEP(S)                                                                        \
-        {                                                                                  \
-            PS::template step<S>(p, buf[S], out);                                           \
-            const int64_t t = t0 + S;                                                      \
-            const int64_t y = s0 + t - 2 * K; /* row emitted by the last stage */          \
-            if (t >= 2 * K && y < s1) {                                                    \
-                if (writer) {                                                              \
-                    store_words<DW>(a.dst + y * a.pitch + col, out);                       \
-                    if (a.slots) {                                                         \
-                        _Pragma("unroll") for (int j = 0; j < DW; ++j) alive += __popc(out[j]); \
-                    }                                                                      \
-                }                                                                          \
-            }                                                                              \
+        // The three rows of this block run through the K stages as a wavefront
+        // (row S is at stage w - S), so every instruction has two independent
+        // neighbours to issue beside it and the DPP read-after-write hazards are
+        // covered without s_nop.
+        uint32_t cur[3][DW];
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int j = 0; j < DW; ++j) cur[s][j] = buf[s][j];
+#pragma unroll
+        for (int w = 0; w < K + 2; ++w) {
+            if (w < K) PS::template stage<0>(p, w, cur[0]);
+            if (w >= 1 && w - 1 < K) PS::template stage<1>(p, w - 1, cur[1]);
+            if (w >= 2 && w - 2 < K) PS::template stage<2>(p, w - 2, cur[2]);
         }
-        GOL_STEP(0)
-        GOL_STEP(1)
-        GOL_STEP(2)
-#undef GOL_STEP
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+            uint32_t (&out)[DW] = cur[S];
+            const int64_t t = t0 + S;
+            const int64_t y = s0 + t - 2 * K;  // row emitted by the last stage
+            if (t >= 2 * K && y < s1) {
+                if constexpr (ALGO == 1) {  // undo the K-bit frame shift
+                    const uint32_t nx0 = from_upper_lane(out[0]);
+#pragma unroll
+                    for (int j = 0; j < DW; ++j)
+                        out[j] = __builtin_amdgcn_alignbit(j == DW - 1 ? nx0 : out[j + 1], out[j], K);
+                }
+                if (writer) {
+                    store_words<DW>(a.dst + y * a.pitch + col, out);
+                    if (a.slots) {
+#pragma unroll
+                        for (int j = 0; j < DW; ++j) alive += __popc(out[j]);
+                    }
+                }
+            }
+        }
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int j = 0; j < DW; ++j) buf[s][j] = nxt[s][j];
+    }
+    if (a.slots) slot_add(a.slots, alive);
+}
+
+// ------------------------------------------------------------------ byte-board step, k turns per launch
+// For boards whose bytes are all 0 or 255 (every board after its first turn):
+// each lane packs 32 bytes of a row into one 32-cell word (bit i = byte i & 1),
+// runs the same K-stage register pipeline as the bit board (shifted frame), and
+// unpacks the result to 0/255 bytes.  HBM traffic: 2 bytes per cell per K turns.
+__device__ __forceinline__ uint32_t pack32(const uint4 lo, const uint4 hi)
+{
+    const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)  // byte q of the word = cells 8q..8q+7
+        b[q] = __builtin_amdgcn_udot4(d[2 * q] & 0x01010101u, 0x08040201u,
+                                      __builtin_amdgcn_udot4(d[2 * q + 1] & 0x01010101u, 0x80402010u, 0u, false),
+                                      false);
+    return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+}
+
+__device__ __forceinline__ void unpack32(const uint32_t w, uint4 &lo, uint4 &hi)
+{
+    uint32_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t n = (w >> (4 * q)) & 0xFu;
+        const uint32_t sp = __umul24(n, 0x00204081u) & 0x01010101u;  // bit i -> byte i
+        o[q] = (sp << 8) - sp;                                       // 0x01 -> 0xFF
+    }
+    lo = make_uint4(o[0], o[1], o[2], o[3]);
+    hi = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+struct BytesKArgs {
+    const uint8_t *top, *mid, *bot;
+    uint8_t *dst;
+    int64_t R, Wd, pitch, row0, rows;  // Wd = W / 32 words, pitch in bytes
+    int32_t strip, ngroups;
+    uint64_t *slots;
+};
+
+template <int K>
+__global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (group >= a.ngroups) return;
+    const int64_t col_raw = (int64_t)group * 62 + (lane - 1);
+    const int64_t col = ((col_raw % a.Wd) + a.Wd) % a.Wd;
+    const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
+    const int64_t s0 = a.row0 + (int64_t)blockIdx.y * a.strip;
+    const int64_t s1 = min(s0 + (int64_t)a.strip, a.row0 + a.rows);
+    const int64_t first_in = s0 - K, last_in = s1 + K - 1;
+    const int64_t nblk = ((s1 - s0) + 2 * K + 2) / 3;
+    const uint8_t *top_adj = a.top + K * a.pitch;
+    const uint8_t *bot_adj = a.bot - a.R * a.pitch;
+    const uint32_t lane_off = (uint32_t)(col * 32);
+    auto load = [&](int64_t y) -> uint32_t {
+        y = y > last_in ? last_in : y;
+        const uint8_t *base = y < 0 ? top_adj : (y >= a.R ? bot_adj : a.mid);
+        const uint4 *p = reinterpret_cast<const uint4 *>(base + y * a.pitch + lane_off);
+        return pack32(p[0], p[1]);
+    };
+    typedef PipeSel<K, 1, 1> PS;
+    typename PS::type p;
+    PS::init(p);
+    uint32_t buf[3][1];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) buf[s][0] = load(first_in + s);
+    uint64_t alive = 0;
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        const int64_t t0 = blk * 3;
+        uint32_t nxt[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) nxt[s] = load(first_in + t0 + 3 + s);
+        uint32_t cur[3][1] = {{buf[0][0]}, {buf[1][0]}, {buf[2][0]}};
+#pragma unroll
+        for (int w = 0; w < K + 2; ++w) {
+            if (w < K) PS::template stage<0>(p, w, cur[0]);
+            if (w >= 1 && w - 1 < K) PS::template stage<1>(p, w - 1, cur[1]);
+            if (w >= 2 && w - 2 < K) PS::template stage<2>(p, w - 2, cur[2]);
+        }
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+            const int64_t t = t0 + S;
+            const int64_t y = s0 + t - 2 * K;
+            if (t >= 2 * K && y < s1) {
+                const uint32_t o = __builtin_amdgcn_alignbit(from_upper_lane(cur[S][0]), cur[S][0], K);
+                if (writer) {
+                    uint4 lo, hi;
+                    unpack32(o, lo, hi);
+                    uint4 *q = reinterpret_cast<uint4 *>(a.dst + y * a.pitch + lane_off);
+                    q[0] = lo;
+                    q[1] = hi;
+                    if (a.slots) alive += __popc(o);
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 3; ++s) buf[s][0] = nxt[s];
     }
     if (a.slots) slot_add(a.slots, alive);
 }
@@ -487,6 +620,18 @@ __global__ void count_nonzero_bytes_kernel(const uint8_t *src, int64_t rows, int
     slot_add(slots, c);
 }
 
+// flag |= 1 if any byte of the rows x W board is neither 0 nor 255
+__global__ void nonbinary_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *flag)
+{
+    const int64_t n = rows * W;
+    uint32_t bad = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t c = bytes[(i / W) * stride + i % W];
+        bad |= (c != 0 && c != 255);
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
 // bytes -> bits: one thread per 32-cell word
 __global__ void pack_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits,
                             int64_t pitch, uint32_t *nonbinary)
@@ -646,7 +791,7 @@ static hipError_t launch_bits_k(int k, const BitsArgs &a, hipStream_t s)
     }
 }
 
-// Step formulation: 0 = horizontal sums first, 1 = vertical sums first.
+// Step formulation: 0 = centred horizontal sums, 1 = shifted frame (left neighbours only).
 // GOL_BITS_ALGO overrides the default (used by tools/sweep.py).
 int golk_bits_algo()
 {
@@ -716,6 +861,37 @@ hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t s
         a.ngroups = 0; a.strip = 0;
         hipLaunchKernelGGL(bytes_step_scalar_kernel, dim3(grid_for((y1 - y0) * W)), dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst, int64_t R,
+                              int64_t W, int64_t pitch, int64_t row0, int64_t rows, int k, int strip, uint64_t *slots,
+                              hipStream_t s)
+{
+    BytesKArgs a;
+    a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
+    a.R = R; a.Wd = W / 32; a.pitch = pitch; a.row0 = row0; a.rows = rows;
+    a.ngroups = (int)((a.Wd + 61) / 62);
+    a.strip = strip > 0 ? strip : golk_auto_strip(rows, a.ngroups, k);
+    a.slots = slots;
+    if (rows <= 0) return hipSuccess;
+    const int nstrips = (int)((rows + a.strip - 1) / a.strip);
+    dim3 grid((a.ngroups + 3) / 4, nstrips);
+    switch (k) {
+    case 1: hipLaunchKernelGGL(bytes_blocked_kernel<1>, grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(bytes_blocked_kernel<2>, grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(bytes_blocked_kernel<4>, grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(bytes_blocked_kernel<8>, grid, dim3(256), 0, s, a); break;
+    case 16: hipLaunchKernelGGL(bytes_blocked_kernel<16>, grid, dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t golk_nonbinary(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *flag, hipStream_t s)
+{
+    hipLaunchKernelGGL(nonbinary_kernel, dim3(grid_for(rows * W, 256, 256 * 16)), dim3(256), 0, s, bytes, rows, W, stride,
+                       flag);
     return hipGetLastError();
 }
 

@@ -90,6 +90,8 @@ SIGNATURES = [
     ("gol_dev_pack", ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
     ("gol_dev_unpack", ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     ("gol_dev_bytes_step", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp]),
+    ("gol_dev_bytes_step_k", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp]),
     ("gol_broker_create", ctypes.c_int, [_P(gol_config), _P(_vp)]),
     ("gol_broker_destroy", None, [_vp]),
     ("gol_broker_run", ctypes.c_int, [_vp, _P(gol_request), _P(gol_response)]),

@@ -160,6 +160,15 @@ int gol_dev_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch,
 int gol_dev_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0,
                        int64_t y1, uint8_t *out, int64_t out_stride, void *stream);
 
+/* k turns (1, 2, 4, 8 or 16) of a byte board whose bytes are all 0 or 255 (every
+ * board after its first turn), W % 32 == 0, stride % 16 == 0, 16-byte aligned
+ * rows; row addressing as gol_dev_bits_step (top/mid/bot are byte rows, pitch
+ * `stride`).  Same results as k exact turns on such boards; 2 bytes of HBM
+ * traffic per cell per k turns.  count_slots as in gol_dev_bits_step. */
+int gol_dev_bytes_step_k(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst, int64_t R,
+                         int64_t W, int64_t stride, int64_t row0, int64_t rows, int32_t k, int32_t strip_rows,
+                         uint64_t *count_slots, void *stream);
+
 /* ---------------------------------------------------------------- RPC service mirror
  * The broker's net/rpc service `Operations` (broker.go:62-277) and the
  * worker's `GameOfLifeOperations` (worker.go:77-86) with the gob field names

@@ -107,7 +107,8 @@ def test_alive_parity_rule(golhip, golden_dir):
 
 # ------------------------------------------------------------------ kernels vs oracle
 @pytest.mark.parametrize("shape", [(64, 64), (128, 256), (100, 192), (37, 320), (1, 64), (2, 128), (3, 64),
-                                   (256, 64 * 65), (16, 16), (48, 80), (20, 100), (7, 33)])
+                                   (256, 64 * 65), (16, 16), (48, 80), (20, 100), (7, 33), (50, 96), (33, 160),
+                                   (300, 32 * 45)])
 @pytest.mark.parametrize("turns", [1, 2, 7, 33])
 def test_random_boards_vs_oracle(golhip, shape, turns):
     H, W = shape
@@ -337,3 +338,29 @@ def test_alive_events_during_run_pause_quit(golhip, golden_dir):
     ops.SuperQuit()
     with pytest.raises(golhip.GolError):
         ops.Run(golhip.Request(World=board, Turns=1, ImageHeight=512, ImageWidth=512, Threads=1))
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
+def test_byte_board_k_turn_kernel(golhip, k):
+    """gol_dev_bytes_step_k (0/255 byte board, k turns per launch) against the oracle, with the
+    torus wrap through top/bot and a split into two launches (row ranges)."""
+    import torch
+    from golhip._lib import check, lib
+    H, W, turns = 203, 32 * 67, 3 * k
+    rng = np.random.default_rng(100 + k)
+    board = (rng.random((H, W)) < 0.4).astype(np.uint8) * 255
+    ref = O.run(board, turns) if H * W * turns < 3_000_000 else None
+    a = torch.from_numpy(board).cuda()
+    b = torch.empty_like(a)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(turns // k):
+        top = a[H - k:]
+        check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W,
+                                         0, 100, k, 0, None, st))
+        check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W,
+                                         100, H - 100, k, 0, None, st))
+        a, b = b, a
+    got = a.cpu().numpy()
+    if ref is None:
+        ref = O.run(board, turns)
+    assert np.array_equal(got, ref)
