@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="weak", choices=["weak", "bit64k", "byte16k"])
-    ap.add_argument("--k", type=int, default=16, help="turns per launch (temporal blocking)")
+    ap.add_argument("--k", type=int, default=0,
+                    help="turns per launch (temporal blocking); 0 = 8 for bit boards, 16 for byte16k")
     ap.add_argument("--cpl", type=int, default=0, help="cells per lane (32/64/128; 0 = library default)")
     ap.add_argument("--strip", type=int, default=0, help="rows per wave strip (0 = auto)")
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
@@ -175,7 +176,7 @@ def run_bits(args, rank, world):
     alg_bytes = BITS_BYTES_PER_UPDATE * krows * W * kk
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     from golhip import lib
-    info = {"turns_per_step": k, "cells_per_lane": args.cpl or 32, "strip_rows": args.strip or "auto"}
+    info = {"turns_per_step": k, "cells_per_lane": args.cpl or "lib default (64)", "strip_rows": args.strip or "auto"}
     pmc = load_pmc(f"{args.workload}:{H}x{W}:n{world}:k{k}:cpl{args.cpl}")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -252,6 +253,8 @@ def run_bytes(args, rank, world):
 
 def main():
     args = parse()
+    if args.k <= 0:
+        args.k = 16 if args.workload == "byte16k" else 8
     rank, world, local = setup(args)
     if args.workload == "byte16k":
         value, dt, cfg, roof, dtype = run_bytes(args, rank, world)

@@ -9,10 +9,10 @@
 // Library defaults for the bit-board step (chosen from the gfx950 sweep recorded
 // in DESIGN.md; overridable per engine through gol_config).
 #ifndef GOL_DEFAULT_K
-#define GOL_DEFAULT_K 16
+#define GOL_DEFAULT_K 8
 #endif
 #ifndef GOL_DEFAULT_DW
-#define GOL_DEFAULT_DW 1
+#define GOL_DEFAULT_DW 2
 #endif
 
 struct gol_engine {

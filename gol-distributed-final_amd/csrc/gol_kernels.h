@@ -8,7 +8,7 @@
 #endif
 
 #ifndef GOL_DEFAULT_ALGO
-#define GOL_DEFAULT_ALGO 0
+#define GOL_DEFAULT_ALGO 1
 #endif
 int golk_bits_algo();
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k);

@@ -228,3 +228,44 @@ class ShardedBoard:
             return torch.cat([p.cpu() for p in parts])
         dist.send(mine, 0, group=self.group)
         return None
+
+
+def _pgm_header(W: int, H: int) -> bytes:
+    """gol/io.go:52-59: "P5\\n<W> <H>\\n255\\n"."""
+    return b"P5\n%d %d\n255\n" % (W, H)
+
+
+def stream_pgm(board: ShardedBoard, sink, chunk_rows: int = 4096) -> None:
+    """Stream the board as the reference's P5 byte layout (gol/io.go:42-87) to `sink` on rank 0.
+
+    Every rank unpacks its rows chunk by chunk on its GPU (bits -> 0/255 bytes) and sends them
+    to rank 0 in row order; rank 0 copies each chunk to the host and calls sink(bytes).  No rank
+    ever holds more than one chunk of bytes, so a 2^20 x 2^20 board (1 TiB of P5) streams with
+    O(chunk) memory.  `sink` is only called on rank 0 (e.g. file.write or hashlib's update)."""
+    W = board.W
+    if board.rank == 0:
+        sink(_pgm_header(W, board.H))
+    for r in range(board.nranks):
+        y0, y1 = partition_rows(board.H, board.nranks, r)
+        for a in range(0, y1 - y0, chunk_rows):
+            n = min(chunk_rows, y1 - y0 - a)
+            if r == board.rank:
+                part = board.kern.unpack(board.board[a:a + n], W)
+                if r != 0:
+                    dist.send(part, 0, group=board.group)
+                    continue
+            elif board.rank == 0:
+                part = torch.empty((n, W), dtype=torch.uint8, device=board.device)
+                dist.recv(part, r, group=board.group)
+            else:
+                continue
+            sink(part.cpu().numpy().tobytes())
+
+
+def write_pgm(board: ShardedBoard, path: str, chunk_rows: int = 4096) -> None:
+    """Write out/<W>x<H>x<Turns>.pgm-style P5 file from a sharded board (rank 0 writes)."""
+    if board.rank == 0:
+        with open(path, "wb") as f:
+            stream_pgm(board, f.write, chunk_rows)
+    else:
+        stream_pgm(board, lambda b: None, chunk_rows)

@@ -86,7 +86,11 @@ def _worker(rank, world, port, H, W, k, turns, seed, q):
         fused = b.fused_count()
         out = (rank, b.y0, b.y1, b.kmax, h0, b.hash(), b.alive_count(), fused)
         full = b.gather_bytes()
-        q.put(out + ((full.numpy() if full is not None else None),))
+        import hashlib
+        from golhip.sharded import stream_pgm
+        h = hashlib.sha256()
+        stream_pgm(b, h.update, chunk_rows=3)
+        q.put(out + ((full.numpy() if full is not None else None), h.hexdigest() if rank == 0 else None))
     finally:
         dist.destroy_process_group()
 
@@ -111,10 +115,12 @@ def test_sharded_matches_oracle(world, H, k, turns):
     words = O.random_words(5, 0, H, W // 64)
     ref = O.bits_run(words, turns)
     res = _run(world, H, W, k, turns)
-    for r, (rank, y0, y1, kmax, h0, h1, count, fused, full) in enumerate(res):
+    for r, (rank, y0, y1, kmax, h0, h1, count, fused, full, digest) in enumerate(res):
         assert (y0, y1) == O.partition(H, world, rank)       # broker.go:172-206 split
         assert kmax <= H // world
         assert h0 == O.hash_words(words)                     # same global board for any N
         assert h1 == O.hash_words(ref)
         assert count == fused == O.popcount_words(ref)
-    assert np.array_equal(res[0][-1], O.unpack(ref))
+    assert np.array_equal(res[0][-2], O.unpack(ref))
+    import hashlib
+    assert res[0][-1] == hashlib.sha256(O.pgm_bytes(O.unpack(ref))).hexdigest()  # gol/io.go P5 bytes
