@@ -266,8 +266,14 @@ struct BitsArgs {
 
 // grid.x: groups of 4 waves along the row; grid.y: strips of output rows.
 // Wave = one column group of 62*DW output words (+1 halo lane each side).
+// Occupancy floor for the register allocator (waves per SIMD); 1 = no constraint.
+#ifndef GOL_MIN_WAVES
+#define GOL_MIN_WAVES(K, DW) 1
+#endif
+
 template <int K, int DW, int ALGO>
-__global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_MIN_WAVES(K, DW), 8)))
+bits_step_kernel(BitsArgs a)
 {
     const int lane = threadIdx.x & 63;
     const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -804,9 +810,12 @@ int golk_bits_algo()
 
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
 {
-    // aim for >= ~8192 waves (32 per CU) while keeping the 2k halo rows small
+    // aim for >= ~8192 waves (32 per CU) but no longer than 64*k rows: the 2k halo rows
+    // then cost <= 1/32 (measured best on the 2^17 x 2^20 torus: 512 rows at k = 8,
+    // 1024 at k = 16)
     int64_t strip = rows * ngroups / 8192;
-    if (strip > 1024) strip = 1024;
+    const int64_t hi = 64 * (int64_t)k;
+    if (strip > hi) strip = hi;
     int64_t lo = 8 * (int64_t)k;
     if (lo < 32) lo = 32;
     if (strip < lo) strip = lo;
