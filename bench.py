@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample length")
+    ap.add_argument("--no-count", action="store_true",
+                    help="do not fuse the alive-cell count (AliveCellsCount) into every launch")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="testing only: every rank uses cuda:0 (multi-rank logic on a 1-GPU box, with --backend gloo)")
@@ -158,25 +160,28 @@ def run_bits(args, rank, world):
     board.load_random(1)
     timer = KernelTimer(["full", "interior"])
     board.launch_hook = timer
+    count = not args.no_count  # AliveCellsCount fused into the last generation of every launch
     for _ in range(args.warmup):
-        board.step(k)
+        board.step(k, count=count)
     barrier(world)
     timer.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        board.step(k)
+        board.step(k, count=count)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     barrier(world)
     timer.enabled = False
     dt = max_over_ranks(dt, world)
+    alive = board.fused_count() if count else None
     cells_total = H * W * (world if nshards == 1 else 1)
     value = cells_total * k * args.steps / dt
     kms, kk, krows = timer.avg()
     alg_bytes = BITS_BYTES_PER_UPDATE * krows * W * kk
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     from golhip import lib
-    info = {"turns_per_step": k, "cells_per_lane": args.cpl or "lib default (64)", "strip_rows": args.strip or "auto"}
+    info = {"turns_per_step": k, "cells_per_lane": args.cpl or "lib default (64)", "strip_rows": args.strip or "auto",
+            "alive_count_every_step": count, "alive_final": alive, "turns_done": board.turn}
     pmc = load_pmc(f"{args.workload}:{H}x{W}:n{world}:k{k}:cpl{args.cpl}")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),

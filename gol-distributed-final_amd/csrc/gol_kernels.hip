@@ -284,22 +284,25 @@ bits_step_kernel(BitsArgs a)
     const int64_t col = ((col_raw % a.Wd) + a.Wd) % a.Wd;
     const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
 
-    const int64_t s0 = a.row0 + (int64_t)blockIdx.y * a.strip;             // first output row
-    const int64_t s1 = min(s0 + (int64_t)a.strip, a.row0 + a.rows);         // end output row
-    const int64_t first_in = s0 - K;                                        // first input row
-    const int64_t last_in = s1 + K - 1;                                     // last input row
-    const int64_t nsteps = (s1 - s0) + 2 * K;
-    const int64_t nblk = (nsteps + 2) / 3;
+    // Row indices are wave-uniform 32-bit values (rows < 2^31), kept in SGPRs.
+    const int R = (int)a.R;
+    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;                   // first output row
+    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));                // end output row
+    const int first_in = s0 - K;                                             // first input row
+    const int last_in = s1 + K - 1;                                          // last input row
+    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
 
     // Input row y lives at base(y) + y*pitch with base = top + k*pitch (y < 0),
-    // mid (0 <= y < R) or bot - R*pitch (y >= R): scalar pointer + per-lane offset.
+    // mid (0 <= y < R) or bot - R*pitch (y >= R): a scalar row pointer plus a
+    // 32-bit per-lane byte offset (global_load ... saddr form).
     const uint32_t *top_adj = a.top + K * a.pitch;
     const uint32_t *bot_adj = a.bot - a.R * a.pitch;
-    const uint32_t lane_off = (uint32_t)col;
-    auto row_ptr = [&](int64_t y) -> const uint32_t * {
+    const uint32_t lane_off = (uint32_t)col * 4u;  // bytes
+    auto row_ptr = [&](int y) -> const uint32_t * {
         y = y > last_in ? last_in : y;  // steps past the end re-read the last row; never stored
-        const uint32_t *base = y < 0 ? top_adj : (y >= a.R ? bot_adj : a.mid);
-        return base + y * a.pitch + lane_off;
+        const uint32_t *base = y < 0 ? top_adj : (y >= R ? bot_adj : a.mid);
+        const char *rb = reinterpret_cast<const char *>(base + (int64_t)y * a.pitch);
+        return reinterpret_cast<const uint32_t *>(rb + lane_off);
     };
 
     typedef PipeSel<K, DW, ALGO> PS;
@@ -311,8 +314,8 @@ bits_step_kernel(BitsArgs a)
     for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + s), buf[s]);
 
     uint64_t alive = 0;
-    for (int64_t blk = 0; blk < nblk; ++blk) {
-        const int64_t t0 = blk * 3;
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int t0 = blk * 3;
         uint32_t nxt[3][DW];
 #pragma unroll
         for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + t0 + 3 + s), nxt[s]);
@@ -335,8 +338,8 @@ bits_step_kernel(BitsArgs a)
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t (&out)[DW] = cur[S];
-            const int64_t t = t0 + S;
-            const int64_t y = s0 + t - 2 * K;  // row emitted by the last stage
+            const int t = t0 + S;
+            const int y = s0 + t - 2 * K;  // row emitted by the last stage
             if (t >= 2 * K && y < s1) {
                 if constexpr (ALGO == 1) {  // undo the K-bit frame shift
                     const uint32_t nx0 = from_upper_lane(out[0]);
@@ -345,7 +348,8 @@ bits_step_kernel(BitsArgs a)
                         out[j] = __builtin_amdgcn_alignbit(j == DW - 1 ? nx0 : out[j + 1], out[j], K);
                 }
                 if (writer) {
-                    store_words<DW>(a.dst + y * a.pitch + col, out);
+                    char *rb = reinterpret_cast<char *>(a.dst + (int64_t)y * a.pitch);
+                    store_words<DW>(reinterpret_cast<uint32_t *>(rb + lane_off), out);
                     if (a.slots) {
 #pragma unroll
                         for (int j = 0; j < DW; ++j) alive += __popc(out[j]);

@@ -47,6 +47,8 @@ for k, c in means.items():
             e["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (256 * 4 * 0.5 * cyc)
     out[k] = e
 json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+if not out:
+    sys.exit(f"no PMC counter rows under {src}")
 main = max(out, key=lambda k: out[k].get("avg_ns_trace") or 0)
 tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 t = json.load(open(tp)) if os.path.exists(tp) else {}
