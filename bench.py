@@ -45,6 +45,8 @@ def parse():
                     help="turns per launch (temporal blocking); 0 = 8 for bit boards, 16 for byte16k")
     ap.add_argument("--cpl", type=int, default=0, help="cells per lane (32/64/128; 0 = library default)")
     ap.add_argument("--strip", type=int, default=0, help="rows per wave strip (0 = auto)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"],
+                    help="bit layout while stepping (auto = band when W %% 1024 == 0; DESIGN.md §4.1)")
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,7 +157,8 @@ def run_bits(args, rank, world):
     if nshards == 1 and world > 1:  # independent replicas: every rank its own board, no collective
         group = [dist.new_group([r]) for r in range(world)][rank]
     board = ShardedBoard(H, W, turns_per_launch=args.k, cells_per_lane=args.cpl, strip_rows=args.strip,
-                         group=group)
+                         group=group, layout=args.layout)
+    layout = "band" if board.use_band else "standard"
     k = board.kmax
     board.load_random(1)
     timer = KernelTimer(["full", "interior"])
@@ -180,9 +183,11 @@ def run_bits(args, rank, world):
     alg_bytes = BITS_BYTES_PER_UPDATE * krows * W * kk
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     from golhip import lib
-    info = {"turns_per_step": k, "cells_per_lane": args.cpl or "lib default (64)", "strip_rows": args.strip or "auto",
+    info = {"turns_per_step": k, "layout": layout,
+            "cells_per_lane": 128 if layout == "band" else (args.cpl or "lib default (64)"),
+            "strip_rows": args.strip or "auto",
             "alive_count_every_step": count, "alive_final": alive, "turns_done": board.turn}
-    pmc = load_pmc(f"{args.workload}:{H}x{W}:n{world}:k{k}:cpl{args.cpl}")
+    pmc = load_pmc(f"{args.workload}:{H}x{W}:n{world}:k{k}:" + ("band" if layout == "band" else f"cpl{args.cpl}"))
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc.get("bytes_per_launch") if pmc else None,
@@ -193,7 +198,8 @@ def run_bits(args, rank, world):
     cfg = {"workload": ("weak-2^17x2^20-per-gpu" if args.workload == "weak" else "bit-65536x65536"),
            "H": H, "W": W, "parallelism": (f"rows{world}" if nshards > 1 else (f"replicas{world}" if world > 1 else "1gpu")),
            **info}
-    return value, dt, cfg, roof, "u32 (bit-packed, 32 cells/word)"
+    dtype = "u32 (bit-packed, 32 cells/word" + (", column-band layout)" if layout == "band" else ")")
+    return value, dt, cfg, roof, dtype
 
 
 def run_bytes(args, rank, world):

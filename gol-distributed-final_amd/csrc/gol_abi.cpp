@@ -111,6 +111,27 @@ static int engine_dev(gol_engine *e)
     return GOL_OK;
 }
 
+// The band layout is a stepping detail: convert on the first step, convert back
+// before anything reads the bits.  Both are one HBM pass (32x32 bit transposes).
+static int to_band(gol_engine *e)
+{
+    if (e->band) return GOL_OK;
+    HIPCHK(golk_band_convert(true, e->bits[e->cur], e->bits[1 - e->cur], e->H, e->Wd, e->pitch, e->pitch, e->stream));
+    e->cur = 1 - e->cur;
+    e->band = true;
+    return GOL_OK;
+}
+
+static int ensure_standard(gol_engine *e)
+{
+    if (!e->bit_mode || !e->band) return GOL_OK;
+    HIPCHK(golk_band_convert(false, e->bits[e->cur], e->bits[1 - e->cur], e->H, e->Wd, e->pitch, e->pitch,
+                             e->stream));
+    e->cur = 1 - e->cur;
+    e->band = false;
+    return GOL_OK;
+}
+
 static void free_bytes(gol_engine *e)
 {
     for (auto &b : e->bytes)
@@ -160,7 +181,19 @@ extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, go
     }
     e->dw = cpl / 32;
     while (e->dw > 1 && (e->Wd % e->dw) != 0) e->dw >>= 1;
+    const int req = cfg ? cfg->cells_per_lane : 0;
+    e->band_dw = req == 64 ? 2 : (req == 128 ? 4 : GOL_BAND_DEFAULT_DW);
     e->strip = cfg ? cfg->strip_rows : 0;
+    const int layout = cfg ? cfg->layout : GOL_LAYOUT_AUTO;
+    if (layout != GOL_LAYOUT_AUTO && layout != GOL_LAYOUT_STANDARD && layout != GOL_LAYOUT_BAND) {
+        delete e;
+        return gol_set_error(GOL_EINVAL, "layout must be GOL_LAYOUT_AUTO, _STANDARD or _BAND");
+    }
+    if (layout == GOL_LAYOUT_BAND && W % 1024 != 0) {
+        delete e;
+        return gol_set_error(GOL_EINVAL, "the band layout needs W %% 1024 == 0");
+    }
+    e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
     int rc = engine_dev(e);
     if (rc == GOL_OK) {
         hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -213,6 +246,7 @@ extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_
     int rc = engine_dev(e);
     if (rc) return rc;
     e->turn = 0;
+    e->band = false;
     if (!e->bit_capable) {
         HIPCHK(hipMemcpy2DAsync(e->bytes[0], e->bstride, world, stride, e->W, e->H, hipMemcpyHostToDevice,
                                 e->stream));
@@ -262,6 +296,7 @@ extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
     if (rc) return rc;
     free_bytes(e);
     e->bit_mode = true;
+    e->band = false;
     e->cur = 0;
     e->turn = 0;
     HIPCHK(golk_random_fill(e->bits[0], e->H, 0, e->W, e->pitch, seed, e->stream));
@@ -299,8 +334,22 @@ int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots)
                 HIPCHK(hipStreamSynchronize(e->stream));
                 free_bytes(e);
                 e->cur = 0;
+                e->band = false;
                 e->bit_mode = true;
             }
+            continue;
+        }
+        if (e->band_capable) {
+            // band layout: a lane of band_dw words keeps 2*ceil(k/band_dw) halo lanes per wave
+            const int k = pick_k(e->k, turns, e->H, e->band_dw);
+            int rc = to_band(e);
+            if (rc) return rc;
+            const uint32_t *mid = e->bits[e->cur];
+            HIPCHK(golk_band_step(mid + (e->H - k) * e->pitch, mid, mid, e->bits[1 - e->cur], e->H, e->Wd, e->pitch,
+                                  0, e->H, k, e->band_dw, e->strip, turns == k ? count_slots : nullptr, e->stream));
+            e->cur = 1 - e->cur;
+            e->turn += k;
+            turns -= k;
             continue;
         }
         const int k = pick_k(e->k, turns, e->H, e->dw);
@@ -361,7 +410,7 @@ extern "C" int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t strid
 {
     if (!e || !out || stride < e->W) return gol_set_error(GOL_EINVAL, "bad store arguments");
     int rc = engine_dev(e);
-    if (rc) return rc;
+    if (rc || (rc = ensure_standard(e))) return rc;
     if (!e->bit_mode) {
         HIPCHK(hipMemcpy2DAsync(out, stride, e->bytes[e->bcur], e->bstride, e->W, e->H, hipMemcpyDeviceToHost,
                                 e->stream));
@@ -383,7 +432,7 @@ extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, i
 {
     if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
     int rc = engine_dev(e);
-    if (rc) return rc;
+    if (rc || (rc = ensure_standard(e))) return rc;
     const bool bm = e->bit_mode;
     const void *board = bm ? (const void *)e->bits[e->cur] : (const void *)e->bytes[e->bcur];
     const int64_t units = bm ? e->Wd : e->W, pitch = bm ? e->pitch : e->bstride;
@@ -423,7 +472,7 @@ extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
 {
     if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
     int rc = engine_dev(e);
-    if (rc) return rc;
+    if (rc || (rc = ensure_standard(e))) return rc;
     if ((rc = ensure_staging(e))) return rc;
     FILE *f = fopen(path, "wb");
     if (!f) return gol_set_error(GOL_EIO, "cannot create %s", path);
@@ -455,7 +504,7 @@ extern "C" int gol_engine_hash(gol_engine *e, uint64_t *hash)
     if (!e || !hash) return gol_set_error(GOL_EINVAL, "bad arguments");
     if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "hash needs W %% 64 == 0");
     int rc = engine_dev(e);
-    if (rc) return rc;
+    if (rc || (rc = ensure_standard(e))) return rc;
     HIPCHK(hipMemsetAsync(e->slots, 0, GOL_COUNT_SLOTS * 8 * sizeof(uint64_t), e->stream));
     const uint32_t *bits = e->bits[e->cur];
     if (!e->bit_mode) {  // loaded non-binary bytes at turn 0: hash the 255-cells
@@ -471,13 +520,17 @@ extern "C" int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lan
                                int32_t *bit_mode)
 {
     if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
-    if (k) *k = e->k;
-    if (cells_per_lane) *cells_per_lane = 32 * e->dw;
+    const bool band = e->bit_mode && e->band_capable;
+    const int dw = band ? e->band_dw : e->dw;
+    const int kk = pick_k(e->k, e->k, e->H, dw);
+    if (k) *k = kk;
+    if (cells_per_lane) *cells_per_lane = 32 * dw;
     if (strip_rows) {
-        const int64_t ng = (e->Wd + 62 * e->dw - 1) / (62 * e->dw);
-        *strip_rows = e->strip > 0 ? e->strip : golk_auto_strip(e->H, ng, pick_k(e->k, e->k, e->H, e->dw));
+        const int64_t u = band ? golk_band_useful_words(kk, dw) : 62 * dw;
+        const int64_t ng = (e->Wd + u - 1) / u;
+        *strip_rows = e->strip > 0 ? e->strip : golk_auto_strip(e->H, ng, kk);
     }
-    if (bit_mode) *bit_mode = e->bit_mode ? 1 : 0;
+    if (bit_mode) *bit_mode = e->bit_mode ? (band ? 2 : 1) : 0;
     return GOL_OK;
 }
 
@@ -485,6 +538,9 @@ extern "C" int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *p
 {
     if (!e || !bits || !pitch) return gol_set_error(GOL_EINVAL, "bad arguments");
     if (!e->bit_mode) return gol_set_error(GOL_ESTATE, "board is not bit-resident");
+    int rc = engine_dev(e);
+    if (rc || (rc = ensure_standard(e))) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
     *bits = e->bits[e->cur];
     *pitch = e->pitch;
     return GOL_OK;
@@ -510,6 +566,35 @@ extern "C" int gol_dev_bits_step(const uint32_t *top, const uint32_t *mid, const
                              (long long)R, (long long)Wd, (long long)pitch, k, dw);
     LAUNCH(golk_bits_step(top, mid, bot, dst, R, Wd, pitch, row0, rows, k, dw, strip_rows, count_slots,
                           (hipStream_t)stream));
+}
+
+extern "C" int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
+                                 int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int32_t k,
+                                 int32_t cells_per_lane, int32_t strip_rows, uint64_t *count_slots, void *stream)
+{
+    const int dw = cells_per_lane == 64 ? 2 : (cells_per_lane == 128 ? 4 : (cells_per_lane <= 0 ? GOL_BAND_DEFAULT_DW : 0));
+    if (!top || !mid || !bot || !dst || R <= 0 || Wd <= 0 || !dw || Wd % dw || pitch < Wd || pitch % dw ||
+        row0 < 0 || rows < 0 || row0 + rows > R || !(k == 1 || k == 2 || k == 4 || k == 8 || (k == 16 && dw == 2)) ||
+        k > R || (((uintptr_t)mid | (uintptr_t)top | (uintptr_t)bot | (uintptr_t)dst) & (4 * dw - 1)))
+        return gol_set_error(GOL_EINVAL, "bad band_step arguments (R=%lld Wd=%lld pitch=%lld k=%d cells_per_lane=%d)",
+                             (long long)R, (long long)Wd, (long long)pitch, k, cells_per_lane);
+    LAUNCH(golk_band_step(top, mid, bot, dst, R, Wd, pitch, row0, rows, k, dw, strip_rows, count_slots,
+                          (hipStream_t)stream));
+}
+
+extern "C" int gol_band_max_k(int32_t cells_per_lane)
+{
+    const int dw = cells_per_lane == 64 ? 2 : (cells_per_lane == 128 ? 4 : (cells_per_lane <= 0 ? GOL_BAND_DEFAULT_DW : 0));
+    return dw == 2 ? 16 : (dw == 4 ? 8 : 0);
+}
+
+extern "C" int gol_dev_band_convert(int32_t to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
+                                    int64_t src_pitch, int64_t dst_pitch, void *stream)
+{
+    if (!src || !dst || src == dst || rows < 0 || Wd <= 0 || Wd % 32 || src_pitch < Wd || dst_pitch < Wd ||
+        (to_band ? dst_pitch : src_pitch) % 4 || (((uintptr_t)(to_band ? dst : src)) & 15))
+        return gol_set_error(GOL_EINVAL, "bad band_convert arguments (Wd=%lld)", (long long)Wd);
+    LAUNCH(golk_band_convert(to_band != 0, src, dst, rows, Wd, src_pitch, dst_pitch, (hipStream_t)stream));
 }
 
 extern "C" int gol_dev_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch,

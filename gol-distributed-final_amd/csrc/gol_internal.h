@@ -24,6 +24,8 @@ struct gol_engine {
     int64_t bstride = 0; // byte-board row pitch in bytes (multiple of 16)
     bool bit_capable = false;  // W % 64 == 0
     bool bit_mode = false;     // board currently lives in bits[cur] (else bytes[bcur])
+    bool band_capable = false; // step the bit board in the band layout (W % 1024 == 0, not disabled)
+    bool band = false;         // bits[cur] currently holds the band layout
     uint32_t *bits[2] = {nullptr, nullptr};
     int cur = 0;
     uint8_t *bytes[2] = {nullptr, nullptr};
@@ -37,6 +39,7 @@ struct gol_engine {
     int64_t turn = 0;
     int k = GOL_DEFAULT_K;
     int dw = GOL_DEFAULT_DW;
+    int band_dw = 4;  // words per lane of the band kernel
     int strip = 0;
 };
 

@@ -15,6 +15,18 @@ int golk_auto_strip(int64_t rows, int64_t ngroups, int k);
 hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
                           int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw,
                           int strip, uint64_t *slots, hipStream_t s);
+// Band layout (bit b of word w = cell b*Wd + w): dw words per lane (2 or 4), k in {1, 2, 4, 8}
+// (and 16 for dw = 2), Wd % dw == 0, pitch % dw == 0, 4*dw-byte aligned rows.
+#ifndef GOL_BAND_DEFAULT_DW
+#define GOL_BAND_DEFAULT_DW 4
+#endif
+hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
+                          int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
+                          uint64_t *slots, hipStream_t s);
+int golk_band_useful_words(int k, int dw);
+// Standard <-> band rows (Wd % 32 == 0), out of place.
+hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
+                             int64_t spitch, int64_t dpitch, hipStream_t s);
 hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0, int64_t y1,
                            uint8_t *out, int64_t out_stride, hipStream_t s);
 hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst, int64_t R,

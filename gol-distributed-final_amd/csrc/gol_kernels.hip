@@ -19,6 +19,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "gol_kernels.h"
 
 namespace golk {
@@ -313,7 +315,7 @@ bits_step_kernel(BitsArgs a)
 #pragma unroll
     for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + s), buf[s]);
 
-    uint64_t alive = 0;
+    uint32_t alive = 0;  // < 2^32: strips are capped at 2^24 rows x 128 cells per lane
     for (int blk = 0; blk < nblk; ++blk) {
         const int t0 = blk * 3;
         uint32_t nxt[3][DW];
@@ -363,6 +365,239 @@ bits_step_kernel(BitsArgs a)
             for (int j = 0; j < DW; ++j) buf[s][j] = nxt[s][j];
     }
     if (a.slots) slot_add(a.slots, alive);
+}
+
+// Store DW words at byte offset voff of a buffer [row, row + nbytes): out-of-range
+// offsets (and nbytes = 0) are dropped by the hardware range check.
+template <int DW>
+__device__ __forceinline__ void store_row_masked(char *row, uint32_t nbytes, uint32_t voff, const uint32_t (&w)[DW])
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, (int)nbytes, 0x00020000);
+    if constexpr (DW == 4) {
+        typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, r, voff, 0, 0);
+    } else if constexpr (DW == 2) {
+        typedef __attribute__((ext_vector_type(2))) uint32_t v2u;
+        __builtin_amdgcn_raw_buffer_store_b64(v2u{w[0], w[1]}, r, voff, 0, 0);
+    } else {
+        static_assert(DW == 4 || DW == 2, "band lanes hold 2 or 4 words");
+    }
+}
+
+// ------------------------------------------------------------------ band-layout bit board
+// Column-band layout: a row is Wd = W/32 words and bit b of word w is cell
+// x = b*Wd + w (32 bands of Wd columns, one per bit).  The horizontal neighbours
+// of a cell are the SAME bit of the neighbouring words, so a generation is pure
+// bitwise logic: no v_alignbit (which issues at half the rate of v_bitop3 on
+// gfx950) and the centre cell is the word itself.  The column
+// torus wraps band b's last column onto band b+1's first: band-space column
+// c = q*Wd + r reads word r rotated right by q (one v_alignbit per word per
+// LOAD, only in the waves that straddle the wrap).  Cost: the horizontal halo
+// is now k words (k columns) instead of one 32-cell word, so a wave of 64 lanes
+// x 4 words keeps 64 - 2*ceil(k/4) lanes of output.
+template <int DW>
+__device__ __forceinline__ void hsum_band(const uint32_t (&c)[DW], uint32_t (&h0)[DW], uint32_t (&h1)[DW])
+{
+    const uint32_t left_in = from_lower_lane(c[DW - 1]);
+    const uint32_t right_in = from_upper_lane(c[0]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+        const uint32_t L = (j == 0) ? left_in : c[j - 1];
+        const uint32_t R = (j == DW - 1) ? right_in : c[j + 1];
+        h0[j] = bitop3<TT_XOR3>(L, c[j], R);
+        h1[j] = bitop3<TT_MAJ>(L, c[j], R);
+    }
+}
+
+template <int K, int DW, int S>
+__device__ __forceinline__ void bstage(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
+{
+    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < DW; ++j) p.cc[g][S][j] = cur[j];
+    hsum_band<DW>(p.cc[g][S], p.h0[g][S], p.h1[g][S]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j)
+        cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j], p.h0[g][S][j],
+                      p.h1[g][S][j], p.cc[g][SM][j]);
+}
+
+__host__ __device__ constexpr int band_halo_lanes(int k, int dw) { return (k + dw - 1) / dw; }
+__host__ __device__ constexpr int band_useful_words(int k, int dw) { return (64 - 2 * band_halo_lanes(k, dw)) * dw; }
+
+#ifndef GOL_BAND_PREFETCH
+#define GOL_BAND_PREFETCH 1  // row blocks loaded ahead of use
+#endif
+#ifndef GOL_BAND_MIN_WAVES
+#define GOL_BAND_MIN_WAVES 1
+#endif
+
+// Same row addressing, strips and fused count as bits_step_kernel; grid.x: groups
+// of 4 waves along the row, grid.y: strips of output rows.  A lane holds DW words.
+template <int K, int DW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_BAND_MIN_WAVES, 8)))
+band_step_kernel(BitsArgs a)
+{
+    constexpr int HL = band_halo_lanes(K, DW);
+    constexpr int U = band_useful_words(K, DW);
+    const int lane = threadIdx.x & 63;
+    const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (group >= a.ngroups) return;
+
+    const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
+    const int64_t q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);  // floor
+    const int64_t col = col_raw - q * a.Wd;
+    const uint32_t rot = (uint32_t)q & 31u;
+    const bool wrap = __ballot(rot != 0) != 0;  // wave-uniform: any lane outside [0, Wd)
+    const bool writer = lane >= HL && lane < 64 - HL && col_raw < a.Wd;
+
+    const int R = (int)a.R;
+    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
+    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
+    const int first_in = s0 - K;
+    const int last_in = s1 + K - 1;
+    constexpr int NB = GOL_BAND_PREFETCH + 1;  // blocks per loop trip (see the ring below)
+    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
+    const int nblk_r = (nblk + NB - 1) / NB * NB;  // trailing blocks re-read the last row, store nothing
+
+    // Scalar row base + 32-bit products (the row pitch in bytes fits 32 bits: W < 2^34 cells).
+    // Every row address is a.mid + (segment displacement + y * pitch): one pointer (the
+    // compiler keeps it in the global address space, so the loads are global_load with
+    // exact vmcnt waits) plus an integer select.  A select between pointer locals can
+    // become an indexed private array (scratch loads in the loop); an integer-to-pointer
+    // cast becomes a flat load (vmcnt(0) + lgkmcnt waits).
+    const int pitch_b = (int)a.pitch * 4;
+    const char *mid_b = reinterpret_cast<const char *>(a.mid);
+    const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch_b;
+    const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch_b;
+    const uint32_t lane_off = (uint32_t)col * 4u;
+    // Stores: buffer stores with the row as the buffer range, so rows that must not be
+    // written (pipeline fill, past the strip) and halo lanes are dropped by the range
+    // check instead of a branch (stores under a branch make the compiler's vmcnt waits
+    // for the NEXT block's rows also wait for these stores).
+    char *dst_b = reinterpret_cast<char *>(a.dst);
+    const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
+    const uint32_t st_off = writer ? lane_off : 0x80000000u;
+    const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
+    auto load_row = [&](int y, uint32_t (&w)[DW]) {
+        y = y > last_in ? last_in : y;
+        const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
+        const char *rb = mid_b + (d + (int64_t)y * pitch_b);
+        load_words<DW>(reinterpret_cast<const uint32_t *>(rb + lane_off), w);
+    };
+    auto unwrap = [&](uint32_t (&w)[DW]) {
+        if (wrap) {
+#pragma unroll
+            for (int j = 0; j < DW; ++j) w[j] = __builtin_amdgcn_alignbit(w[j], w[j], rot);
+        }
+    };
+
+    Pipe<K, DW> p;
+    PipeSel<K, DW, 0>::init(p);
+
+    // Row blocks in flight: a ring of PF+1 three-row buffers; block b lives in ring[b % (PF+1)]
+    // and is loaded PF blocks ahead of use.  The block loop is unrolled by PF+1 so the ring
+    // index is static: no register copies, and the loads are waited for just before their
+    // first use (a copy at the loop end would also wait for that block's stores: gfx9 has
+    // one in-order vmcnt for loads and stores).
+    constexpr int PF = GOL_BAND_PREFETCH;
+    uint32_t ring[NB][3][DW];
+#pragma unroll
+    for (int b = 0; b < PF; ++b)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) load_row(first_in + 3 * b + s, ring[b][s]);
+    // Three empty-range stores (dropped) so that the loop is entered with the same
+    // memory-counter history as its back edge (loads, then a block's 3 stores): the
+    // compiler then waits for the block's rows with vmcnt(6), not vmcnt(3).
+#pragma unroll
+    for (int s = 0; s < 3; ++s) store_row_masked<DW>(dst_b, 0u, st_off, ring[0][s]);
+
+    uint32_t alive = 0;  // < 2^32: strips are capped at 2^24 rows x 128 cells per lane
+    for (int blk0 = 0; blk0 < nblk_r; blk0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int t0 = (blk0 + u) * 3;
+#pragma unroll
+            for (int s = 0; s < 3; ++s) load_row(first_in + t0 + 3 * PF + s, ring[(u + PF) % NB][s]);
+            uint32_t (&cur)[3][DW] = ring[u];
+#pragma unroll
+            for (int s = 0; s < 3; ++s) unwrap(cur[s]);
+#pragma unroll
+            for (int w = 0; w < K + 2; ++w) {
+                if (w < K) bstage<K, DW, 0>(p, w, cur[0]);
+                if (w >= 1 && w - 1 < K) bstage<K, DW, 1>(p, w - 1, cur[1]);
+                if (w >= 2 && w - 2 < K) bstage<K, DW, 2>(p, w - 2, cur[2]);
+            }
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+                const int t = t0 + S;
+                const int y = s0 + t - 2 * K;
+                const bool row_ok = t >= 2 * K && y < s1;  // wave-uniform
+                store_row_masked<DW>(dst_b + (int64_t)(row_ok ? y : s0) * pitch_b, row_ok ? row_bytes : 0u, st_off,
+                                     cur[S]);
+                if (a.slots) {
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int j = 0; j < DW; ++j) c += __popc(cur[S][j]);
+                    alive += c & (row_ok ? st_mask : 0u);
+                }
+            }
+        }
+    }
+    if (a.slots) slot_add(a.slots, alive);
+}
+
+// 32 x 32 bit-matrix transpose in registers: afterwards x[i] bit b = (before) x[b] bit i.
+__device__ __forceinline__ void transpose32(uint32_t (&x)[32])
+{
+    uint32_t m = 0x0000FFFFu;
+#pragma unroll
+    for (int j = 16; j != 0; j >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if (k & j) continue;
+            const uint32_t t = ((x[k] >> j) ^ x[k + j]) & m;
+            x[k + j] ^= t;
+            x[k] ^= t << j;
+        }
+        m ^= m << (j >> 1);
+    }
+}
+
+// Standard bit rows (word s bit i = cell 32s + i) -> band rows, or back.  One lane per
+// (row, m): the 32 standard words m, m + Wm, ..., m + 31*Wm (Wm = Wd/32) hold exactly
+// the cells of band words 32m .. 32m+31, so the conversion is one 32x32 transpose.
+template <bool TO_BAND>
+__global__ void band_convert_kernel(const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wm, int64_t spitch,
+                                    int64_t dpitch)
+{
+    const int64_t n = rows * Wm;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / Wm, m = i % Wm;
+        uint32_t x[32];
+        if (TO_BAND) {
+            const uint32_t *s = src + y * spitch + m;
+#pragma unroll
+            for (int b = 0; b < 32; ++b) x[b] = s[b * Wm];
+        } else {
+            const uint4 *s = reinterpret_cast<const uint4 *>(src + y * spitch + 32 * m);
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const uint4 q = s[v];
+                x[4 * v] = q.x; x[4 * v + 1] = q.y; x[4 * v + 2] = q.z; x[4 * v + 3] = q.w;
+            }
+        }
+        transpose32(x);
+        if (TO_BAND) {
+            uint4 *d = reinterpret_cast<uint4 *>(dst + y * dpitch + 32 * m);
+#pragma unroll
+            for (int v = 0; v < 8; ++v) d[v] = make_uint4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]);
+        } else {
+            uint32_t *d = dst + y * dpitch + m;
+#pragma unroll
+            for (int b = 0; b < 32; ++b) d[b * Wm] = x[b];
+        }
+    }
 }
 
 // ------------------------------------------------------------------ byte-board step, k turns per launch
@@ -770,6 +1005,9 @@ __global__ void row_counts_bytes_kernel(const uint8_t *bytes, int64_t rows, int6
 // ------------------------------------------------------------------ launchers
 using namespace golk;
 
+// Rows per wave strip are capped so a lane's 32-bit alive count cannot overflow.
+constexpr int GOL_MAX_STRIP = 1 << 24;
+
 static inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 16)
 {
     int64_t g = (n + block - 1) / block;
@@ -836,7 +1074,7 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
     a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
     a.ngroups = (int)((Wd + 62 * dw - 1) / (62 * dw));
-    a.strip = strip > 0 ? strip : golk_auto_strip(rows, a.ngroups, k);
+    a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
     a.slots = slots;
     if (rows <= 0) return hipSuccess;
     const int algo = golk_bits_algo();
@@ -849,6 +1087,53 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     case 9: return launch_bits_k<4, 1>(k, a, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+template <int DW>
+static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s)
+{
+    switch (k) {
+    case 1: hipLaunchKernelGGL((band_step_kernel<1, DW>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((band_step_kernel<2, DW>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((band_step_kernel<4, DW>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((band_step_kernel<8, DW>), grid, dim3(256), 0, s, a); break;
+    case 16: if constexpr (DW <= 2) { hipLaunchKernelGGL((band_step_kernel<16, DW>), grid, dim3(256), 0, s, a); break; }
+             return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
+                          int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
+                          uint64_t *slots, hipStream_t s)
+{
+    if (rows <= 0) return hipSuccess;
+    BitsArgs a;
+    a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
+    a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
+    const int U = band_useful_words(k, dw);
+    a.ngroups = (int)((Wd + U - 1) / U);
+    a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
+    a.slots = slots;
+    dim3 grid((a.ngroups + 3) / 4, (int)((rows + a.strip - 1) / a.strip));
+    if (dw == 2) return launch_band<2>(k, grid, a, s);
+    if (dw == 4) return launch_band<4>(k, grid, a, s);
+    return hipErrorInvalidValue;
+}
+
+int golk_band_useful_words(int k, int dw) { return band_useful_words(k, dw); }
+
+hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
+                             int64_t spitch, int64_t dpitch, hipStream_t s)
+{
+    const int64_t Wm = Wd / 32;
+    const dim3 g(grid_for(rows * Wm, 256, 256 * 64));
+    if (to_band)
+        hipLaunchKernelGGL(band_convert_kernel<true>, g, dim3(256), 0, s, src, dst, rows, Wm, spitch, dpitch);
+    else
+        hipLaunchKernelGGL(band_convert_kernel<false>, g, dim3(256), 0, s, src, dst, rows, Wm, spitch, dpitch);
+    return hipGetLastError();
 }
 
 hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0, int64_t y1,

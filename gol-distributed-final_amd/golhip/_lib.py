@@ -22,6 +22,8 @@ GOL_EFORMAT = -5
 GOL_ESTATE = -6
 GOL_EQUIT = -7
 GOL_COUNT_SLOTS = 256
+GOL_LAYOUT_AUTO, GOL_LAYOUT_STANDARD, GOL_LAYOUT_BAND = 0, 1, 2
+LAYOUTS = {"auto": GOL_LAYOUT_AUTO, "standard": GOL_LAYOUT_STANDARD, "band": GOL_LAYOUT_BAND}
 
 _NAMES = {
     GOL_EINVAL: "EINVAL", GOL_EHIP: "EHIP", GOL_ENOMEM: "ENOMEM", GOL_EIO: "EIO",
@@ -38,7 +40,7 @@ class GolError(RuntimeError):
 class gol_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
                 ("strip_rows", ctypes.c_int32), ("cells_per_lane", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 4)]
+                ("layout", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 class gol_request(ctypes.Structure):
@@ -92,6 +94,10 @@ SIGNATURES = [
     ("gol_dev_bytes_step", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp]),
     ("gol_dev_bytes_step_k", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp]),
+    ("gol_dev_band_step", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
+    ("gol_band_max_k", ctypes.c_int, [_i32]),
+    ("gol_dev_band_convert", ctypes.c_int, [_i32, _vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     ("gol_broker_create", ctypes.c_int, [_P(gol_config), _P(_vp)]),
     ("gol_broker_destroy", None, [_vp]),
     ("gol_broker_run", ctypes.c_int, [_vp, _P(gol_request), _P(gol_response)]),

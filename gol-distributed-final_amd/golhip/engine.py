@@ -10,15 +10,15 @@ import ctypes
 
 import numpy as np
 
-from ._lib import check, gol_config, lib
+from ._lib import LAYOUTS, check, gol_config, lib
 
 
 class Engine:
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
-                 strip_rows: int = 0, device: int = -1):
+                 strip_rows: int = 0, device: int = -1, layout: str = "auto"):
         self.H, self.W = int(height), int(width)
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, strip_rows=strip_rows,
-                         cells_per_lane=cells_per_lane)
+                         cells_per_lane=cells_per_lane, layout=LAYOUTS[layout])
         h = ctypes.c_void_p()
         check(lib().gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -93,7 +93,7 @@ class Engine:
         check(lib().gol_engine_info(self._h, ctypes.byref(k), ctypes.byref(cpl), ctypes.byref(strip),
                                     ctypes.byref(bm)))
         return {"turns_per_launch": k.value, "cells_per_lane": cpl.value, "strip_rows": strip.value,
-                "bit_mode": bool(bm.value)}
+                "bit_mode": bool(bm.value), "layout": {0: None, 1: "standard", 2: "band"}[bm.value]}
 
     def device_bits(self):
         p = ctypes.c_void_p()

@@ -34,8 +34,9 @@ VALID_K = (16, 8, 4, 2, 1)
 class HipKernels:
     """Launch the C-ABI device kernels on torch CUDA tensors and torch's current stream."""
 
-    def __init__(self, cells_per_lane: int = 0, strip_rows: int = 0):
+    def __init__(self, cells_per_lane: int = 0, strip_rows: int = 0, band_cells_per_lane: int = 0):
         self.cells_per_lane = cells_per_lane
+        self.band_cells_per_lane = band_cells_per_lane  # 0 = library default
         self.strip_rows = strip_rows
         lib()  # fail loudly now if the library is missing
 
@@ -48,6 +49,19 @@ class HipKernels:
         check(lib().gol_dev_bits_step(top.data_ptr(), mid.data_ptr(), bot.data_ptr(), dst.data_ptr(), R,
                                       self.Wd, pitch, row0, rows, k, self.cells_per_lane, self.strip_rows,
                                       slots.data_ptr() if slots is not None else None, self._stream()))
+
+    def band_step(self, top, mid, bot, dst, row0: int, rows: int, k: int, slots=None) -> None:
+        R, pitch = mid.shape
+        check(lib().gol_dev_band_step(top.data_ptr(), mid.data_ptr(), bot.data_ptr(), dst.data_ptr(), R,
+                                      self.Wd, pitch, row0, rows, k, self.band_cells_per_lane, self.strip_rows,
+                                      slots.data_ptr() if slots is not None else None, self._stream()))
+
+    def band_max_k(self) -> int:
+        return lib().gol_band_max_k(self.band_cells_per_lane)
+
+    def band_convert(self, to_band: bool, src, dst) -> None:
+        check(lib().gol_dev_band_convert(1 if to_band else 0, src.data_ptr(), dst.data_ptr(), src.shape[0], self.Wd,
+                                         src.shape[1], dst.shape[1], self._stream()))
 
     def random_fill(self, dst, grow0: int, W: int, seed: int) -> None:
         rows, pitch = dst.shape
@@ -77,9 +91,13 @@ class ShardedBoard:
     """A W-wide, H-tall bit-packed torus, rows sharded over the ranks of `group`."""
 
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 8, cells_per_lane: int = 0,
-                 strip_rows: int = 0, device=None, kernels=None, group=None):
+                 strip_rows: int = 0, device=None, kernels=None, group=None, layout: str = "auto"):
         if width % 64:
             raise ValueError("the sharded bit board needs W % 64 == 0")
+        if layout not in ("auto", "standard", "band"):
+            raise ValueError(f"unknown layout {layout!r}")
+        if layout == "band" and width % 1024:
+            raise ValueError("the band layout needs W % 1024 == 0")
         self.H, self.W = int(height), int(width)
         self.group = group
         if dist.is_available() and dist.is_initialized():
@@ -91,13 +109,19 @@ class ShardedBoard:
         min_rows = self.H // self.nranks  # smallest shard (broker.go:172-206 split)
         if min_rows < 1:
             raise ValueError(f"{self.nranks} ranks cannot shard {self.H} rows")
-        self.kmax = max(k for k in VALID_K if k <= max(1, min(turns_per_launch, min_rows)))
         self.Wd = self.W // 32
         self.pitch = (self.Wd + 3) // 4 * 4
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if kernels is None else torch.device("cpu")
         self.device = torch.device(device)
         self.kern = kernels if kernels is not None else HipKernels(cells_per_lane, strip_rows)
+        # Band layout: stepped shift-free; converted back before any read.
+        self.use_band = layout != "standard" and self.W % 1024 == 0 and hasattr(self.kern, "band_step")
+        if layout == "band" and not self.use_band:
+            raise ValueError("these kernels have no band-layout step")
+        kcap = self.kern.band_max_k() if self.use_band and hasattr(self.kern, "band_max_k") else (8 if self.use_band else 16)
+        self.kmax = max(k for k in VALID_K if k <= max(1, min(turns_per_launch, min_rows, kcap)))
+        self.band = False  # buf[cur] holds the band layout
         self.kern.Wd = self.Wd
         z = dict(dtype=torch.int32, device=self.device)
         self.buf = [torch.zeros((self.R, self.pitch), **z), torch.zeros((self.R, self.pitch), **z)]
@@ -119,13 +143,27 @@ class ShardedBoard:
     def load_random(self, seed: int) -> None:
         """Synthetic torus: identical global board for every rank count."""
         self.kern.random_fill(self.board, self.y0, self.W, seed)
+        self.band = False
         self.turn = 0
+
+    def _convert(self, to_band: bool) -> None:
+        if self.band == to_band:
+            return
+        self.kern.band_convert(to_band, self.board, self.buf[1 - self.cur])
+        self.cur = 1 - self.cur
+        self.band = to_band
+
+    def standard(self) -> torch.Tensor:
+        """This rank's rows in the standard bit layout (converts back from the band layout)."""
+        self._convert(False)
+        return self.board
 
     def load_bytes(self, board_rows) -> None:
         """Load this rank's rows [y0, y1) from a (R, W) uint8 tensor of 0/255 bytes."""
         if tuple(board_rows.shape) != (self.R, self.W):
             raise ValueError("expected this rank's (R, W) rows")
         self.kern.pack(board_rows.to(self.device).contiguous(), self.board)
+        self.band = False
         self.turn = 0
 
     # ------------------------------------------------------------ stepping
@@ -158,12 +196,15 @@ class ShardedBoard:
         hook = self.launch_hook
         if hook is not None:
             hook(kind, k, rows, True)
-        self.kern.bits_step(top, self.board, bot, dst, row0, rows, k, slots)
+        step = self.kern.band_step if self.band else self.kern.bits_step
+        step(top, self.board, bot, dst, row0, rows, k, slots)
         if hook is not None:
             hook(kind, k, rows, False)
 
     def step(self, turns: int, count: bool = False) -> None:
         """Advance exactly `turns` turns (k-turn launches + halo exchange)."""
+        if turns > 0 and self.use_band:
+            self._convert(True)
         while turns > 0:
             k = max(kk for kk in VALID_K if kk <= min(self.kmax, turns))
             last = turns == k
@@ -211,12 +252,12 @@ class ShardedBoard:
     def hash(self) -> int:
         """Order-independent board hash (oracle_hash_words), summed over shards."""
         self.slots.zero_()
-        self.kern.hash(self.board, self.y0, self.slots)
+        self.kern.hash(self.standard(), self.y0, self.slots)
         return self._allreduce(self._slot_sum())
 
     def gather_bytes(self):
         """Whole board as (H, W) uint8 0/255 on rank 0 (None elsewhere).  Small boards only."""
-        mine = self.kern.unpack(self.board, self.W)
+        mine = self.kern.unpack(self.standard(), self.W)
         if self.nranks == 1:
             return mine.cpu()
         parts = [torch.empty((partition_rows(self.H, self.nranks, r)[1] - partition_rows(self.H, self.nranks, r)[0],
@@ -243,6 +284,7 @@ def stream_pgm(board: ShardedBoard, sink, chunk_rows: int = 4096) -> None:
     ever holds more than one chunk of bytes, so a 2^20 x 2^20 board (1 TiB of P5) streams with
     O(chunk) memory.  `sink` is only called on rank 0 (e.g. file.write or hashlib's update)."""
     W = board.W
+    rows = board.standard()
     if board.rank == 0:
         sink(_pgm_header(W, board.H))
     for r in range(board.nranks):
@@ -250,7 +292,7 @@ def stream_pgm(board: ShardedBoard, sink, chunk_rows: int = 4096) -> None:
         for a in range(0, y1 - y0, chunk_rows):
             n = min(chunk_rows, y1 - y0 - a)
             if r == board.rank:
-                part = board.kern.unpack(board.board[a:a + n], W)
+                part = board.kern.unpack(rows[a:a + n], W)
                 if r != 0:
                     dist.send(part, 0, group=board.group)
                     continue

@@ -78,12 +78,21 @@ int gol_partition_rows(int64_t H, int64_t parts, int64_t i, int64_t *y0, int64_t
  * HBM and is stepped in k-turn launches. */
 typedef struct gol_engine gol_engine;
 
+/* Bit-board layout used while stepping.  STANDARD: word s of a row holds cells
+ * 32s .. 32s+31.  BAND: word w holds, at bit b, cell b*(W/32) + w (32 column
+ * bands), which makes a generation shift-free.  AUTO picks
+ * BAND when W % 1024 == 0.  The layout is internal: every reader (store,
+ * alive list, PGM, hash, device_bits) sees the standard layout. */
+#define GOL_LAYOUT_AUTO 0
+#define GOL_LAYOUT_STANDARD 1
+#define GOL_LAYOUT_BAND 2
 typedef struct gol_config {
     int32_t device;           /* HIP device ordinal; -1 = current device */
     int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
     int32_t strip_rows;       /* rows per wave strip; 0 = automatic */
     int32_t cells_per_lane;   /* 32, 64 or 128 bits per lane; 0 = automatic */
-    int32_t reserved[4];
+    int32_t layout;           /* bit-board layout while stepping: GOL_LAYOUT_* */
+    int32_t reserved[3];
 } gol_config;
 
 int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, gol_engine **out);
@@ -169,6 +178,22 @@ int gol_dev_bytes_step_k(const uint8_t *top, const uint8_t *mid, const uint8_t *
                          int64_t W, int64_t stride, int64_t row0, int64_t rows, int32_t k, int32_t strip_rows,
                          uint64_t *count_slots, void *stream);
 
+/* k turns of a BAND-layout bit board (bit b of word w = cell b*Wd + w); row
+ * addressing and count_slots as gol_dev_bits_step.  cells_per_lane: 64 or 128
+ * (2 or 4 words per lane; 0 = library default); k in {1, 2, 4, 8}, and 16 with
+ * 64 cells per lane; Wd and pitch multiples of the words per lane, rows aligned
+ * to 4 bytes x words per lane.  Same cells as gol_dev_bits_step on the standard
+ * layout, with no bit shifts in the generation. */
+int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
+                      int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int32_t k,
+                      int32_t cells_per_lane, int32_t strip_rows, uint64_t *count_slots, void *stream);
+/* Largest k gol_dev_band_step accepts for this cells_per_lane (0 = default);
+ * 0 if cells_per_lane is not supported. */
+int gol_band_max_k(int32_t cells_per_lane);
+/* Convert rows x Wd words between the standard and the band layout (to_band
+ * != 0: standard -> band), out of place; Wd % 32 == 0 (W % 1024 == 0). */
+int gol_dev_band_convert(int32_t to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
+                         int64_t src_pitch, int64_t dst_pitch, void *stream);
 /* ---------------------------------------------------------------- RPC service mirror
  * The broker's net/rpc service `Operations` (broker.go:62-277) and the
  * worker's `GameOfLifeOperations` (worker.go:77-86) with the gob field names

@@ -15,6 +15,7 @@ small numpy restatement plus the PGM codec of the reference:
 * ``pgm_bytes``         gol/io.go:42-87  ("P5\\n<W> <H>\\n255\\n" + H*W bytes)
 * ``np_next_state``     numpy restatement of the same rule (cross-check)
 * ``bits_run``          word-parallel restatement for long runs
+* ``to_band`` / ``from_band``  the column-band bit layout (numpy restatement)
 
 Pinned against the reference's own fixtures in ``tests/golden`` (copied from
 /root/reference/check and /root/reference/images); see tests/test_oracle.py.
@@ -181,6 +182,27 @@ def bits_run(words: np.ndarray, turns: int, with_counts: bool = False):
     if rc != 0:
         raise ValueError("oracle_bits_run failed")
     return (w, counts[:turns]) if with_counts else w
+
+
+def to_band(words: np.ndarray) -> np.ndarray:
+    """Standard bit rows (uint64, 64 cells per word) -> band rows as uint32 words:
+    band word w of a row holds at bit b the cell x = b*Wd + w (Wd = W/32).  This is
+    the layout definition of gol_dev_band_convert, restated."""
+    cells = unpack(words) != 0                      # (H, W) bool, x = column
+    H, W = cells.shape
+    Wd = W // 32
+    bands = cells.reshape(H, 32, Wd).astype(np.uint64)  # [y, b, w]
+    shifts = np.arange(32, dtype=np.uint64)[None, :, None]
+    return (bands << shifts).sum(axis=1).astype(np.uint32)
+
+
+def from_band(band: np.ndarray) -> np.ndarray:
+    """Inverse of to_band: band uint32 rows -> standard uint64 rows."""
+    band = np.ascontiguousarray(band, dtype=np.uint32)
+    H, Wd = band.shape
+    bits = (band[:, None, :] >> np.arange(32, dtype=np.uint32)[None, :, None]) & 1  # [y, b, w]
+    cells = bits.reshape(H, 32 * Wd).astype(np.uint8) * 255
+    return pack(cells)
 
 
 # ---------------------------------------------------------------- PGM codec (gol/io.go)

@@ -140,6 +140,68 @@ def test_kernel_variants_vs_bit_oracle(golhip, k, cpl):
         assert np.array_equal(e.store_bytes(), O.unpack(ref))
 
 
+@pytest.mark.parametrize("k,cpl", [(1, 128), (2, 128), (4, 128), (8, 128), (1, 64), (4, 64), (8, 64), (16, 64)])
+@pytest.mark.parametrize("shape", [(300, 1024), (97, 2048), (64, 3072), (33, 8192), (5, 1024)])
+def test_band_layout_vs_bit_oracle(golhip, k, cpl, shape):
+    """Band-layout kernel (bit b of word w = cell b*W/32 + w) for every (k, words per lane):
+    W = 1024 makes one wave span the 32-word row several times (column wrap by rotation)."""
+    H, W = shape
+    seed = 100 + k + W
+    words = O.random_words(seed, 0, H, W // 64)
+    ref, counts = O.bits_run(words, 45, with_counts=True)
+    with golhip.Engine(H, W, device=0, turns_per_launch=k, cells_per_lane=cpl, layout="band") as e:
+        e.load_random(seed)
+        info = e.info()
+        assert info["layout"] == "band" and info["cells_per_lane"] == cpl
+        assert info["turns_per_launch"] == min(k, 16 if H >= 16 else 4 if H >= 4 else 1)
+        e.step(20)
+        assert e.alive_count() == counts[19]  # popcount on the band layout
+        e.step(25)
+        assert e.hash() == O.hash_words(ref)
+        assert np.array_equal(e.store_bytes(), O.unpack(ref))
+        e.step(3)  # back to band after a read
+        assert e.alive_count() == O.popcount_words(O.bits_run(ref, 3))
+
+
+def test_band_layout_standard_agree(golhip):
+    """layout=band and layout=standard engines agree on a board loaded from bytes, on the alive
+    list (row-major), the PGM bytes and the counts."""
+    H, W = 200, 4096
+    rng = np.random.default_rng(8)
+    board = (rng.random((H, W)) < 0.3).astype(np.uint8) * 255
+    out = []
+    for layout in ("standard", "band"):
+        with golhip.Engine(H, W, device=0, layout=layout) as e:
+            e.load_bytes(board)
+            e.step(29)
+            out.append((e.store_bytes(), e.alive_cells(), e.alive_count(), e.info()["layout"]))
+    assert out[0][3] == "standard" and out[1][3] == "band"
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]
+    assert np.array_equal(out[1][0], O.unpack(O.bits_run(O.pack(board), 29)))
+
+
+def test_band_convert_device(golhip):
+    """gol_dev_band_convert against the numpy restatement of the layout (padded pitch)."""
+    import torch
+    from golhip.sharded import HipKernels
+    rows, W = 9, 4096
+    Wd = W // 32
+    words = O.random_words(4, 0, rows, W // 64)
+    src = torch.zeros((rows, Wd + 8), dtype=torch.int32, device="cuda")
+    src[:, :Wd] = torch.from_numpy(words.view(np.int32)).cuda()
+    band = torch.full((rows, Wd + 4), -1, dtype=torch.int32, device="cuda")
+    back = torch.zeros_like(src)
+    k = HipKernels()
+    k.Wd = Wd
+    k.band_convert(True, src, band)
+    k.band_convert(False, band, back)
+    torch.cuda.synchronize()
+    assert np.array_equal(band[:, :Wd].cpu().numpy().view(np.uint32), O.to_band(words))
+    assert (band[:, Wd:] == -1).all()  # padding untouched
+    assert np.array_equal(back[:, :Wd].cpu().numpy().view(np.uint64), words)
+
+
 @pytest.mark.parametrize("strip", [1, 5, 32, 97])
 def test_strip_sizes(golhip, strip):
     H, W = 211, 64 * 9
@@ -263,14 +325,16 @@ def test_tiled_board_matches_small_torus(golhip):
 
 
 def test_bench_size_k_and_shard_invariance(golhip):
-    """2^17 x 2^20 (the bench's per-GPU torus): k=1, k=8 and k=16 launches give the same board
-    hash, and the fused popcount equals the popcount kernel."""
+    """2^17 x 2^20 (the bench's per-GPU torus): k=1, 8 and 16 launches on the standard layout
+    and k=1, 8 on the band layout give the same board hash, and the fused popcount equals the
+    popcount kernel."""
     import torch
     from golhip.sharded import ShardedBoard
     H, W, turns = 1 << 17, 1 << 20, 16
     hashes = []
-    for k in (1, 8, 16):
-        b = ShardedBoard(H, W, turns_per_launch=k)
+    for layout, k in (("standard", 1), ("standard", 8), ("standard", 16), ("band", 1), ("band", 8)):
+        b = ShardedBoard(H, W, turns_per_launch=k, layout=layout)
+        assert b.use_band == (layout == "band")
         b.load_random(1)
         b.step(turns, count=True)
         torch.cuda.synchronize()

@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, H, W, k, turns, q):
+def _worker(rank, world, port, H, W, k, turns, q, layout="auto"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "gol-distributed-final_amd")]
@@ -34,7 +34,7 @@ def _worker(rank, world, port, H, W, k, turns, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from golhip.sharded import ShardedBoard
-        b = ShardedBoard(H, W, turns_per_launch=k)
+        b = ShardedBoard(H, W, turns_per_launch=k, layout=layout)
         b.load_random(3)
         b.step(turns, count=True)
         torch.cuda.synchronize()
@@ -43,13 +43,15 @@ def _worker(rank, world, port, H, W, k, turns, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,k,turns", [(2, 1024, 8, 37), (3, 1000, 16, 50), (4, 515, 4, 21)])
-def test_sharded_gpu_ranks_match_oracle(world, H, k, turns):
+@pytest.mark.parametrize("world,H,W,k,turns", [(2, 1024, 64 * 40, 8, 37), (3, 1000, 64 * 40, 16, 50),
+                                                (4, 515, 64 * 40, 4, 21),
+                                                # W % 1024 == 0: band layout, halos are band rows
+                                                (2, 1024, 2048, 8, 37), (3, 301, 3072, 4, 22)])
+def test_sharded_gpu_ranks_match_oracle(world, H, W, k, turns):
     import torch
     import torch.multiprocessing as mp
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    W = 64 * 40
     ref = O.bits_run(O.random_words(3, 0, H, W // 64), turns)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

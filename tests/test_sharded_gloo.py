@@ -44,6 +44,27 @@ class OracleKernels:
         if slots is not None:
             slots[0] += O.popcount_words(out)
 
+    def band_step(self, top, mid, bot, dst, row0, rows, k, slots=None):
+        # same as bits_step on the band layout: restate through the standard layout
+        R = mid.shape[0]
+        Wd = self.Wd
+        rows_in = []
+        for y in range(row0 - k, row0 + rows + k):
+            src = top[y + k] if y < 0 else (bot[y - R] if y >= R else mid[y])
+            rows_in.append(src.numpy().view(np.uint32)[:Wd])
+        std = O.from_band(np.stack(rows_in))
+        out = O.bits_run(std, k)[k:k + rows]
+        dst.numpy().view(np.uint32)[row0:row0 + rows, :Wd] = O.to_band(out)
+        if slots is not None:
+            slots[0] += O.popcount_words(out)
+
+    def band_convert(self, to_band, src, dst):
+        a = np.ascontiguousarray(src.numpy().view(np.uint32)[:, :self.Wd])
+        if to_band:
+            dst.numpy().view(np.uint32)[:, :self.Wd] = O.to_band(a.view(np.uint64))
+        else:
+            dst.numpy().view(np.uint32)[:, :self.Wd] = O.from_band(a).view(np.uint32)
+
     def random_fill(self, dst, grow0, W, seed):
         rows = dst.shape[0]
         words = O.random_words(seed, grow0, rows, W // 64)
@@ -80,6 +101,7 @@ def _worker(rank, world, port, H, W, k, turns, seed, q):
     try:
         from golhip.sharded import ShardedBoard
         b = ShardedBoard(H, W, turns_per_launch=k, kernels=OracleKernels(), device="cpu")
+        assert b.use_band == (W % 1024 == 0)
         b.load_random(seed)
         h0 = b.hash()
         b.step(turns, count=True)
@@ -109,9 +131,11 @@ def _run(world, H, W, k, turns, seed=5):
     return sorted(res, key=lambda r: r[0])
 
 
-@pytest.mark.parametrize("world,H,k,turns", [(2, 64, 8, 21), (3, 50, 4, 13), (4, 67, 2, 9), (2, 9, 4, 6)])
-def test_sharded_matches_oracle(world, H, k, turns):
-    W = 128
+@pytest.mark.parametrize("world,H,W,k,turns", [(2, 64, 128, 8, 21), (3, 50, 128, 4, 13), (4, 67, 128, 2, 9),
+                                                (2, 9, 128, 4, 6),
+                                                # W % 1024 == 0: stepped in the band layout
+                                                (2, 40, 1024, 8, 19), (3, 31, 2048, 4, 11)])
+def test_sharded_matches_oracle(world, H, W, k, turns):
     words = O.random_words(5, 0, H, W // 64)
     ref = O.bits_run(words, turns)
     res = _run(world, H, W, k, turns)
