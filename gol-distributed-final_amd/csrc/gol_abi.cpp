@@ -200,11 +200,13 @@ extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, go
         if (he == hipSuccess) he = hipMalloc(&e->slots, GOL_COUNT_SLOTS * 8 * sizeof(uint64_t));
         if (he == hipSuccess) he = hipMalloc(&e->flag, sizeof(uint32_t));
         if (he == hipSuccess && e->bit_capable) {
-            for (auto &b : e->bits) {
-                he = hipMalloc(&b, H * e->pitch * sizeof(uint32_t));
+            const int64_t rows = H + 2 * GOL_GHOST_ROWS;
+            for (int i = 0; i < 2; ++i) {
+                he = hipMalloc(&e->bits_alloc[i], rows * e->pitch * sizeof(uint32_t));
                 if (he != hipSuccess) break;
-                he = hipMemset(b, 0, H * e->pitch * sizeof(uint32_t));
+                he = hipMemset(e->bits_alloc[i], 0, rows * e->pitch * sizeof(uint32_t));
                 if (he != hipSuccess) break;
+                e->bits[i] = e->bits_alloc[i] + GOL_GHOST_ROWS * e->pitch;
             }
             e->bit_mode = true;
         }
@@ -229,7 +231,7 @@ extern "C" void gol_engine_destroy(gol_engine *e)
 {
     if (!e) return;
     (void)hipSetDevice(e->device);
-    for (auto &b : e->bits)
+    for (auto &b : e->bits_alloc)
         if (b) (void)hipFree(b);
     free_bytes(e);
     if (e->slots) (void)hipFree(e->slots);
@@ -344,9 +346,15 @@ int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots)
             const int k = pick_k(e->k, turns, e->H, e->band_dw);
             int rc = to_band(e);
             if (rc) return rc;
-            const uint32_t *mid = e->bits[e->cur];
-            HIPCHK(golk_band_step(mid + (e->H - k) * e->pitch, mid, mid, e->bits[1 - e->cur], e->H, e->Wd, e->pitch,
-                                  0, e->H, k, e->band_dw, e->strip, turns == k ? count_slots : nullptr, e->stream));
+            // torus wrap rows into the halo rows right above / below the board (contiguous rows)
+            uint32_t *mid = e->bits[e->cur];
+            const size_t hb = (size_t)k * e->pitch * sizeof(uint32_t);
+            HIPCHK(hipMemcpyAsync(mid - k * e->pitch, mid + (e->H - k) * e->pitch, hb, hipMemcpyDeviceToDevice,
+                                  e->stream));
+            HIPCHK(hipMemcpyAsync(mid + e->H * e->pitch, mid, hb, hipMemcpyDeviceToDevice, e->stream));
+            HIPCHK(golk_band_step(mid - k * e->pitch, mid, mid + e->H * e->pitch, e->bits[1 - e->cur], e->H, e->Wd,
+                                  e->pitch, 0, e->H, k, e->band_dw, e->strip, turns == k ? count_slots : nullptr,
+                                  e->stream));
             e->cur = 1 - e->cur;
             e->turn += k;
             turns -= k;

@@ -15,6 +15,10 @@
 #define GOL_DEFAULT_DW 2
 #endif
 
+// Halo rows kept above and below each bit buffer: the band kernel reads the torus wrap
+// from them as contiguous rows (its CONTIG path, no per-row segment select).
+#define GOL_GHOST_ROWS 16
+
 struct gol_engine {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -26,7 +30,8 @@ struct gol_engine {
     bool bit_mode = false;     // board currently lives in bits[cur] (else bytes[bcur])
     bool band_capable = false; // step the bit board in the band layout (W % 1024 == 0, not disabled)
     bool band = false;         // bits[cur] currently holds the band layout
-    uint32_t *bits[2] = {nullptr, nullptr};
+    uint32_t *bits[2] = {nullptr, nullptr};       // row 0 of each bit buffer
+    uint32_t *bits_alloc[2] = {nullptr, nullptr}; // allocations: GOL_GHOST_ROWS halo rows above and below
     int cur = 0;
     uint8_t *bytes[2] = {nullptr, nullptr};
     int bcur = 0;

@@ -453,7 +453,9 @@ __host__ __device__ constexpr int band_useful_words(int k, int dw) { return (64 
 
 // Same row addressing, strips and fused count as bits_step_kernel; grid.x: groups
 // of 4 waves along the row, grid.y: strips of output rows.  A lane holds DW words.
-template <int K, int DW>
+// CONTIG: top == mid - K*pitch and bot == mid + R*pitch (halo rows stored right above and
+// below the shard), so input row y is simply mid + y*pitch: no per-row segment select.
+template <int K, int DW, bool CONTIG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_BAND_MIN_WAVES, 8)))
 band_step_kernel(BitsArgs a)
 {
@@ -500,7 +502,7 @@ band_step_kernel(BitsArgs a)
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
     auto load_row = [&](int y, uint32_t (&w)[DW]) {
         y = y > last_in ? last_in : y;
-        const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
+        const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
         const char *rb = mid_b + (d + (int64_t)y * pitch_b);
         load_words<DW>(reinterpret_cast<const uint32_t *>(rb + lane_off), w);
     };
@@ -1139,15 +1141,15 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     }
 }
 
-template <int DW>
+template <int DW, bool C>
 static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s)
 {
     switch (k) {
-    case 1: hipLaunchKernelGGL((band_step_kernel<1, DW>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((band_step_kernel<2, DW>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((band_step_kernel<4, DW>), grid, dim3(256), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((band_step_kernel<8, DW>), grid, dim3(256), 0, s, a); break;
-    case 16: if constexpr (DW <= 2) { hipLaunchKernelGGL((band_step_kernel<16, DW>), grid, dim3(256), 0, s, a); break; }
+    case 1: hipLaunchKernelGGL((band_step_kernel<1, DW, C>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((band_step_kernel<2, DW, C>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((band_step_kernel<4, DW, C>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((band_step_kernel<8, DW, C>), grid, dim3(256), 0, s, a); break;
+    case 16: if constexpr (DW <= 2) { hipLaunchKernelGGL((band_step_kernel<16, DW, C>), grid, dim3(256), 0, s, a); break; }
              return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
     }
@@ -1167,8 +1169,9 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
     a.slots = slots;
     dim3 grid((a.ngroups + 3) / 4, (int)((rows + a.strip - 1) / a.strip));
-    if (dw == 2) return launch_band<2>(k, grid, a, s);
-    if (dw == 4) return launch_band<4>(k, grid, a, s);
+    const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
+    if (dw == 2) return contig ? launch_band<2, true>(k, grid, a, s) : launch_band<2, false>(k, grid, a, s);
+    if (dw == 4) return contig ? launch_band<4, true>(k, grid, a, s) : launch_band<4, false>(k, grid, a, s);
     return hipErrorInvalidValue;
 }
 

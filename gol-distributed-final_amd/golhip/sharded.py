@@ -124,10 +124,12 @@ class ShardedBoard:
         self.band = False  # buf[cur] holds the band layout
         self.kern.Wd = self.Wd
         z = dict(dtype=torch.int32, device=self.device)
-        self.buf = [torch.zeros((self.R, self.pitch), **z), torch.zeros((self.R, self.pitch), **z)]
+        # Each buffer keeps kmax halo rows right above and below the shard's R rows, so the
+        # halo (received from the neighbours, or the torus wrap on one rank) is contiguous
+        # with the board: the band kernel then addresses row y as board + y*pitch.
+        self._store = [torch.zeros((self.R + 2 * self.kmax, self.pitch), **z) for _ in range(2)]
+        self.buf = [t[self.kmax:self.kmax + self.R] for t in self._store]
         self.cur = 0
-        self.ghost_top = torch.zeros((self.kmax, self.pitch), **z)
-        self.ghost_bot = torch.zeros((self.kmax, self.pitch), **z)
         self.slots = torch.zeros(GOL_COUNT_SLOTS * 8, dtype=torch.int64, device=self.device)
         self.turn = 0
         self.prev = (self.rank - 1) % self.nranks
@@ -167,10 +169,19 @@ class ShardedBoard:
         self.turn = 0
 
     # ------------------------------------------------------------ stepping
+    def halo(self, k: int):
+        """(top, bot): the k halo rows right above row 0 and right below row R-1 of buf[cur]."""
+        st, km, R = self._store[self.cur], self.kmax, self.R
+        return st[km - k:km], st[km + R:km + R + k]
+
     def _exchange(self, k: int):
         cur = self.board
+        top_h, bot_h = self.halo(k)
         if self.nranks == 1:
-            return None
+            # torus wrap: the last k rows above row 0, the first k rows below row R-1
+            top_h.copy_(cur[self.R - k:])
+            bot_h.copy_(cur[:k])
+            return []
         g = self.group
         if self.device.type == "cuda" and dist.get_backend(g) == "gloo":
             # gloo has no device P2P: stage the halo rows through host memory (used to test
@@ -181,13 +192,13 @@ class ShardedBoard:
                    dist.P2POp(dist.isend, down, self.next, g), dist.P2POp(dist.irecv, top, self.prev, g)]
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
-            self.ghost_bot[:k].copy_(bot)
-            self.ghost_top[:k].copy_(top)
+            bot_h.copy_(bot)
+            top_h.copy_(top)
             return []
         ops = [dist.P2POp(dist.isend, cur[:k], self.prev, g),
-               dist.P2POp(dist.irecv, self.ghost_bot[:k], self.next, g),
+               dist.P2POp(dist.irecv, bot_h, self.next, g),
                dist.P2POp(dist.isend, cur[self.R - k:], self.next, g),
-               dist.P2POp(dist.irecv, self.ghost_top[:k], self.prev, g)]
+               dist.P2POp(dist.irecv, top_h, self.prev, g)]
         return dist.batch_isend_irecv(ops)
 
     def _launch(self, kind, top, bot, dst, row0, rows, k, slots):
@@ -211,22 +222,23 @@ class ShardedBoard:
             slots = self.slots if (count and last) else None
             if slots is not None:
                 slots.zero_()
-            cur, dst = self.board, self.buf[1 - self.cur]
+            dst = self.buf[1 - self.cur]
             R = self.R
+            top, bot = self.halo(k)
+            reqs = self._exchange(k)
             if self.nranks == 1:
-                self._launch("full", cur[R - k:], cur, dst, 0, R, k, slots)
+                self._launch("full", top, bot, dst, 0, R, k, slots)
             else:
-                reqs = self._exchange(k)
                 interior = R >= 3 * k
-                if interior:
-                    self._launch("interior", self.ghost_top, self.ghost_bot, dst, k, R - 2 * k, k, slots)
+                if interior:  # rows [k, R-k) need no halo: overlaps the exchange
+                    self._launch("interior", top, bot, dst, k, R - 2 * k, k, slots)
                 for r in reqs:
                     r.wait()
                 if interior:
-                    self._launch("boundary", self.ghost_top, self.ghost_bot, dst, 0, k, k, slots)
-                    self._launch("boundary", self.ghost_top, self.ghost_bot, dst, R - k, k, k, slots)
+                    self._launch("boundary", top, bot, dst, 0, k, k, slots)
+                    self._launch("boundary", top, bot, dst, R - k, k, k, slots)
                 else:
-                    self._launch("boundary", self.ghost_top, self.ghost_bot, dst, 0, R, k, slots)
+                    self._launch("boundary", top, bot, dst, 0, R, k, slots)
             self.cur = 1 - self.cur
             self.turn += k
             turns -= k

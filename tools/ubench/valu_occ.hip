@@ -19,7 +19,9 @@ __global__ void __launch_bounds__(256) k(uint32_t *out, uint64_t *cyc, int iters
 #pragma unroll
             for (int c = 0; c < CH; ++c) {
                 if (MODE == 0) x[c] = __builtin_amdgcn_bitop3_b32(x[c], y[c], z[c], 0x96);
-                if (MODE == 1) x[c] = x[c] ^ y[c];  // VOP2, 2 VGPR sources
+                if (MODE == 1) asm volatile("v_xor_b32_e32 %0, %1, %0" : "+v"(x[c]) : "v"(y[c]));  // VOP2, 4 bytes
+                if (MODE == 3) asm volatile("v_xor_b32_e64 %0, %1, %0" : "+v"(x[c]) : "v"(y[c]));  // VOP3, 8 bytes
+                if (MODE == 4) asm volatile("v_not_b32_e32 %0, %0" : "+v"(x[c]));                  // VOP1
                 if (MODE == 2) {                   // one DPP move per 4 bitop3
                     x[c] = __builtin_amdgcn_bitop3_b32(x[c], y[c], z[c], 0x96);
                     if ((r & 3) == 0) y[c] = __builtin_amdgcn_mov_dpp(x[c], 0x138, 0xf, 0xf, true);
@@ -71,10 +73,12 @@ void run(int wps, const char *name)
 
 int main()
 {
-    for (int w : {1, 2, 3, 4, 8}) {
+    for (int w : {1, 2, 4}) {
         run<4, 0>(w, "bitop3 (3 vgpr)");
         run<8, 0>(w, "bitop3 (3 vgpr)");
-        run<8, 1>(w, "v_xor_b32 (vop2)");
+        run<8, 1>(w, "v_xor_b32_e32 (vop2, 4 B)");
+        run<8, 3>(w, "v_xor_b32_e64 (vop3, 8 B)");
+        run<8, 4>(w, "v_not_b32_e32 (vop1)");
         run<8, 2>(w, "bitop3 + dpp/4");
     }
     return 0;
