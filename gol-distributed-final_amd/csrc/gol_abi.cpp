@@ -95,11 +95,14 @@ extern "C" int gol_next_state_slab(const uint8_t *world, int64_t H, int64_t W, i
 }
 
 // ------------------------------------------------------------------ engine
-static int pick_k(int want, int64_t remaining, int64_t H, int dw)
+// Turns per launch: the largest supported k <= want, remaining turns and rows.  k = 12 is
+// the band layout's split pipeline (4 words per lane, band = true); k = 16 needs <= 2 words.
+static int pick_k(int want, int64_t remaining, int64_t H, int dw, bool band = false)
 {
-    static const int ks[] = {16, 8, 4, 2, 1};
+    static const int ks[] = {16, 12, 8, 4, 2, 1};
     for (int k : ks) {
         if (k == 16 && dw > 2) continue;
+        if (k == 12 && !(band && dw == 4)) continue;
         if (k <= want && k <= remaining && k <= H) return k;
     }
     return 1;
@@ -204,7 +207,9 @@ extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, go
             for (int i = 0; i < 2; ++i) {
                 he = hipMalloc(&e->bits_alloc[i], rows * e->pitch * sizeof(uint32_t));
                 if (he != hipSuccess) break;
-                he = hipMemset(e->bits_alloc[i], 0, rows * e->pitch * sizeof(uint32_t));
+                // on the engine's stream: it is non-blocking, so a null-stream memset could still
+                // be running when the first load or fill kernel writes the board
+                he = hipMemsetAsync(e->bits_alloc[i], 0, rows * e->pitch * sizeof(uint32_t), e->stream);
                 if (he != hipSuccess) break;
                 e->bits[i] = e->bits_alloc[i] + GOL_GHOST_ROWS * e->pitch;
             }
@@ -212,9 +217,10 @@ extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, go
         }
         if (he == hipSuccess && !e->bit_capable) {
             rc = alloc_bytes(e);
-            if (rc == GOL_OK) he = hipMemset(e->bytes[0], 0, H * e->bstride);
+            if (rc == GOL_OK) he = hipMemsetAsync(e->bytes[0], 0, H * e->bstride, e->stream);
             e->bit_mode = false;
         }
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
         if (he != hipSuccess)
             rc = gol_set_error(he == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP, "engine allocation: %s",
                                hipGetErrorString(he));
@@ -343,7 +349,7 @@ int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots)
         }
         if (e->band_capable) {
             // band layout: a lane of band_dw words keeps 2*ceil(k/band_dw) halo lanes per wave
-            const int k = pick_k(e->k, turns, e->H, e->band_dw);
+            const int k = pick_k(e->k, turns, e->H, e->band_dw, true);
             int rc = to_band(e);
             if (rc) return rc;
             // torus wrap rows into the halo rows right above / below the board (contiguous rows)
@@ -530,7 +536,7 @@ extern "C" int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lan
     if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
     const bool band = e->bit_mode && e->band_capable;
     const int dw = band ? e->band_dw : e->dw;
-    const int kk = pick_k(e->k, e->k, e->H, dw);
+    const int kk = pick_k(e->k, e->k, e->H, dw, band);
     if (k) *k = kk;
     if (cells_per_lane) *cells_per_lane = 32 * dw;
     if (strip_rows) {
@@ -582,7 +588,8 @@ extern "C" int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const
 {
     const int dw = cells_per_lane == 64 ? 2 : (cells_per_lane == 128 ? 4 : (cells_per_lane <= 0 ? GOL_BAND_DEFAULT_DW : 0));
     if (!top || !mid || !bot || !dst || R <= 0 || Wd <= 0 || !dw || Wd % dw || pitch < Wd || pitch % dw ||
-        row0 < 0 || rows < 0 || row0 + rows > R || !(k == 1 || k == 2 || k == 4 || k == 8 || (k == 16 && dw == 2)) ||
+        row0 < 0 || rows < 0 || row0 + rows > R ||
+        !(k == 1 || k == 2 || k == 4 || k == 8 || (k == 16 && dw == 2) || (k == 12 && dw == 4)) ||
         k > R || (((uintptr_t)mid | (uintptr_t)top | (uintptr_t)bot | (uintptr_t)dst) & (4 * dw - 1)))
         return gol_set_error(GOL_EINVAL, "bad band_step arguments (R=%lld Wd=%lld pitch=%lld k=%d cells_per_lane=%d)",
                              (long long)R, (long long)Wd, (long long)pitch, k, cells_per_lane);
@@ -593,7 +600,7 @@ extern "C" int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const
 extern "C" int gol_band_max_k(int32_t cells_per_lane)
 {
     const int dw = cells_per_lane == 64 ? 2 : (cells_per_lane == 128 ? 4 : (cells_per_lane <= 0 ? GOL_BAND_DEFAULT_DW : 0));
-    return dw == 2 ? 16 : (dw == 4 ? 8 : 0);
+    return dw == 2 ? 16 : (dw == 4 ? 12 : 0);
 }
 
 extern "C" int gol_dev_band_convert(int32_t to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,

@@ -24,6 +24,11 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
                           uint64_t *slots, hipStream_t s);
 int golk_band_useful_words(int k, int dw);
+// Split-pipeline band kernel: k = 8/12/16 as 2/3/4 waves x 4 stages.
+#ifndef GOL_BAND_SPLIT_DEFAULT
+#define GOL_BAND_SPLIT_DEFAULT 0
+#endif
+int golk_band_split_enabled();
 // Standard <-> band rows (Wd % 32 == 0), out of place.
 hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
                              int64_t spitch, int64_t dpitch, hipStream_t s);

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "gol_kernels.h"
 
@@ -441,9 +442,29 @@ __device__ __forceinline__ void bstage(Pipe<K, DW> &p, const int g, uint32_t (&c
     for (int j = 0; j < DW; ++j) cur[j] = bitop3<TT_MUX>(t0[j], e1[j], e2[j]);
 }
 
+// Same stage with the rule evaluated word by word (fewer live temporaries than bstage).
+template <int K, int DW, int S>
+__device__ __forceinline__ void bstage_seq(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
+{
+    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < DW; ++j) p.cc[g][S][j] = cur[j];
+    hsum_band<DW>(p.cc[g][S], p.h0[g][S], p.h1[g][S]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j)
+        cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j], p.h0[g][S][j],
+                      p.h1[g][S][j], p.cc[g][SM][j]);
+}
+
 __host__ __device__ constexpr int band_halo_lanes(int k, int dw) { return (k + dw - 1) / dw; }
 __host__ __device__ constexpr int band_useful_words(int k, int dw) { return (64 - 2 * band_halo_lanes(k, dw)) * dw; }
 
+#ifndef GOL_SPLIT_KW
+#define GOL_SPLIT_KW 3  // stages per wave of the split pipeline
+#endif
+#ifndef GOL_SPLIT_MIN_WAVES
+#define GOL_SPLIT_MIN_WAVES 4
+#endif
 #ifndef GOL_BAND_PREFETCH
 #define GOL_BAND_PREFETCH 1  // row blocks loaded ahead of use
 #endif
@@ -566,6 +587,320 @@ band_step_kernel(BitsArgs a)
         }
     }
     if (a.slots) slot_add(a.slots, alive);
+}
+
+// ------------------------------------------------------------------ band layout, split pipeline
+// The K stages of band_step_kernel split over P waves of one workgroup, KW = K/P stages
+// each: wave w runs stages [w*KW, (w+1)*KW) and hands every block of 3 rows to wave w+1
+// through LDS.  A wave then holds 5*KW*4 pipeline VGPRs instead of 5*K*4, which fits
+// 4 waves per SIMD: v_bitop3_b32 issues at ~1.9 SIMD cycles per wave64 instruction at 4
+// waves per SIMD against ~2.8 at 2 (tools/ubench/valu_dep.hip), and K = 12 keeps HBM
+// at ~1/12 of a board pass per turn.  Wave 0 stages the input rows HBM -> LDS with
+// global_load_lds (no VGPRs); every wave reads its input block with ds_read_b128.
+// Periods: in period j wave w works on block j - w; one workgroup barrier per period
+// (LDS slots are double-buffered by block parity).
+template <int DW>
+__device__ __forceinline__ void lds_read_row(const uint32_t *slot, int lane, uint32_t (&w)[DW])
+{
+    static_assert(DW == 4, "the split pipeline keeps 4 words per lane");
+    const uint4 v = reinterpret_cast<const uint4 *>(slot)[lane];
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+}
+template <int DW>
+__device__ __forceinline__ void lds_write_row(uint32_t *slot, int lane, const uint32_t (&w)[DW])
+{
+    reinterpret_cast<uint4 *>(slot)[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int KW, int P, bool CONTIG>
+__global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(GOL_SPLIT_MIN_WAVES, 8)))
+band_split_kernel(BitsArgs a)
+{
+    constexpr int DW = 4;
+    constexpr int K = KW * P;
+    constexpr int HL = band_halo_lanes(K, DW);
+    constexpr int U = band_useful_words(K, DW);
+    constexpr int ROW = 64 * DW;  // uint32 per LDS row slot (1 KiB)
+    // LDS: input slots of wave 0 (filled by global_load_lds; one array per block parity so
+    // the compiler sees that a staging DMA never aliases the slot being read) and the
+    // hand-off slots of waves 0 .. P-2, [parity][row of block][lane][DW words].
+    __shared__ uint32_t lds_in0[3][ROW], lds_in1[3][ROW];
+    __shared__ uint32_t lds_x[P - 1][2][3][ROW];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // pipeline position
+    const int group = blockIdx.x;
+
+    const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
+    const int64_t q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
+    const int64_t col = col_raw - q * a.Wd;
+    const uint32_t rot = (uint32_t)q & 31u;
+    const bool wrap = __ballot(rot != 0) != 0;
+    const bool writer = lane >= HL && lane < 64 - HL && col_raw < a.Wd;
+
+    const int R = (int)a.R;
+    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
+    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
+    const int first_in = s0 - K;
+    const int last_in = s1 + K - 1;
+    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
+
+    const int pitch_b = (int)a.pitch * 4;
+    const char *mid_b = reinterpret_cast<const char *>(a.mid);
+    const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch_b;
+    const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch_b;
+    const uint32_t lane_off = (uint32_t)col * 4u;
+    char *dst_b = reinterpret_cast<char *>(a.dst);
+    const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
+    const uint32_t st_off = writer ? lane_off : 0x80000000u;
+
+    // wave 0: the 3 rows of block b -> slot (global_load_lds: lane l writes 16 B at l*16)
+    auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            int y = first_in + 3 * b + s;
+            y = y > last_in ? last_in : y;
+            const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
+            const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
+        }
+    };
+
+    Pipe<KW, DW> p;
+    PipeSel<KW, DW, 0>::init(p);
+    if (wv == 0) {
+        stage_in(0, lds_in0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    uint32_t alive = 0;
+    // One period: this wave's block b = period - wv.  PAR = period parity (static, so wave
+    // 0's input slot and staging slot are distinct arrays).
+    auto period_body = [&](const int period, auto par) {
+        constexpr int PAR = decltype(par)::value;
+        const int b = period - wv;
+        if (b >= 0 && b < nblk) {
+            if (wv == 0 && b + 1 < nblk) stage_in(b + 1, PAR ? lds_in0 : lds_in1);  // slot freed last period
+            const uint32_t *src = wv == 0 ? &(PAR ? lds_in1 : lds_in0)[0][0] : &lds_x[wv == 0 ? 0 : wv - 1][b & 1][0][0];
+            uint32_t *dstx = &lds_x[wv < P - 1 ? wv : 0][b & 1][0][0];
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+                uint32_t cur[DW];
+                lds_read_row<DW>(src + S * ROW, lane, cur);
+                if (wv == 0 && wrap) {
+#pragma unroll
+                    for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
+                }
+                // one row through this wave's KW stages (at 4 waves per SIMD a dependent VALU
+                // op issues as fast as an independent one: no wavefront interleave needed)
+#pragma unroll
+                for (int g = 0; g < KW; ++g) {
+                    if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
+                    if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
+                    if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+                }
+                if (wv == P - 1) {
+                    const int t = 3 * b + S;
+                    const int y = s0 + t - 2 * K;
+                    const bool row_ok = t >= 2 * K && y < s1;
+                    store_row_masked<DW>(dst_b + (int64_t)(row_ok ? y : s0) * pitch_b, row_ok ? row_bytes : 0u,
+                                         st_off, cur);
+                    if (a.slots) {
+                        uint32_t c = 0;
+#pragma unroll
+                        for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
+                        alive += (row_ok && writer) ? c : 0u;
+                    }
+                } else {
+                    lds_write_row<DW>(dstx + S * ROW, lane, cur);
+                }
+            }
+        }
+        if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next block staged
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    const int nper = nblk + P - 1;
+    int period = 0;
+    for (; period + 1 < nper; period += 2) {
+        period_body(period, std::integral_constant<int, 0>());
+        period_body(period + 1, std::integral_constant<int, 1>());
+    }
+    if (period < nper) period_body(period, std::integral_constant<int, 0>());
+    if (a.slots && wv == P - 1) slot_add(a.slots, alive);
+}
+
+// Flag-synchronised split pipeline (no workgroup barriers): wave w consumes ring w (ring
+// 0 = the input rows, staged by wave 0 itself with global_load_lds) and produces ring
+// w+1; each ring has NS slots of one block (3 rows).  ready[e] = blocks published into
+// ring e, consumed[e] = blocks taken out of it.  A producer may fill slot b % NS once its
+// consumer has taken block b - NS; a consumer may read block b once ready > b.  The chain
+// has no cycle, and every spin is bounded (a protocol fault ends the wave, and the parity
+// tests then fail, instead of hanging the GPU).
+#ifndef GOL_PIPE_SLOTS
+#define GOL_PIPE_SLOTS 3
+#endif
+// LDS accesses of the pipeline are inline asm: the compiler treats a global_load_lds in
+// flight as a pending LDS write and would put vmcnt(0) before every LDS access it can see
+// (which, on the storing wave, also waits for its HBM stores).  Each read waits for its own
+// result (lgkmcnt(0)); the LDS latency is hidden by the other waves of the SIMD.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((ext_vector_type(4))) uint32_t v4u32;
+__device__ __forceinline__ v4u32 lds_rd128(const lds_u32 *p)
+{
+    v4u32 r;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_wr128(lds_u32 *p, v4u32 v)
+{
+    asm volatile("ds_write_b128 %0, %1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ int lds_rd32(const lds_u32 *p)
+{
+    int r;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_wr32(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
+__device__ __forceinline__ bool spin_until_ge(const lds_u32 *f, int v)
+{
+    for (int n = 0; n < (1 << 22); ++n) {
+        if (__builtin_amdgcn_readfirstlane(lds_rd32(f)) >= v) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+template <int KW, int P, bool CONTIG>
+__global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(GOL_SPLIT_MIN_WAVES, 8)))
+band_pipe_kernel(BitsArgs a)
+{
+    constexpr int DW = 4;
+    constexpr int K = KW * P;
+    constexpr int HL = band_halo_lanes(K, DW);
+    constexpr int U = band_useful_words(K, DW);
+    constexpr int ROW = 64 * DW;
+    constexpr int NS = GOL_PIPE_SLOTS;
+    __shared__ uint32_t ring[P][NS][3][ROW];
+    __shared__ int ready[P], consumed[P];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = blockIdx.x;
+
+    const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
+    const int64_t q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
+    const int64_t col = col_raw - q * a.Wd;
+    const uint32_t rot = (uint32_t)q & 31u;
+    const bool wrap = __ballot(rot != 0) != 0;
+    const bool writer = lane >= HL && lane < 64 - HL && col_raw < a.Wd;
+
+    const int R = (int)a.R;
+    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
+    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
+    const int first_in = s0 - K;
+    const int last_in = s1 + K - 1;
+    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
+
+    const int pitch_b = (int)a.pitch * 4;
+    const char *mid_b = reinterpret_cast<const char *>(a.mid);
+    const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch_b;
+    const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch_b;
+    const uint32_t lane_off = (uint32_t)col * 4u;
+    char *dst_b = reinterpret_cast<char *>(a.dst);
+    const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
+    const uint32_t st_off = writer ? lane_off : 0x80000000u;
+
+    // wave 0: block b -> ring[0][b % NS] (global_load_lds).  The slot is an argument: a lambda
+    // that captures a __shared__ array silently loses the kernel's host-side stub.
+    auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            int y = first_in + 3 * b + s;
+            y = y > last_in ? last_in : y;
+            const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
+            const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
+        }
+    };
+
+    if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
+    __syncthreads();
+    lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
+    lds_u32 *const ready_l = (lds_u32 *)&ready[0];
+    lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
+    constexpr int SLOT = 3 * ROW;  // uint32 per slot (one block)
+    auto slot_row = [&](int e, int b, int S) { return ring_l + (e * NS + b % NS) * SLOT + S * ROW + lane * 4; };
+
+    Pipe<KW, DW> p;
+    PipeSel<KW, DW, 0>::init(p);
+    if (wv == 0) {
+        stage_in(0, ring[0][0]);
+        if (nblk > 1) stage_in(1, ring[0][1 % NS]);
+    }
+    uint32_t alive = 0;
+    bool ok = true;
+    for (int b = 0; b < nblk && ok; ++b) {
+        // input block b
+        if (wv == 0) {
+            if (b + 1 < nblk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // block b+1 may stay in flight
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            ok = spin_until_ge(ready_l + wv, b + 1);
+            if (!ok) break;
+        }
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+            uint32_t cur[DW];
+            {
+                const v4u32 v = lds_rd128(slot_row(wv, b, S));  // waited: block b row S is in VGPRs
+                cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
+            }
+            if (S == 2) {
+                if (wv == 0) {
+                    if (b + 2 < nblk) stage_in(b + 2, ring[0][(b + 2) % NS]);  // refills slot (b-1) % NS
+                } else if (lane == 0) {
+                    lds_wr32(consumed_l + wv, b + 1);
+                }
+            }
+            if (wv == 0 && wrap) {
+#pragma unroll
+                for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
+            }
+#pragma unroll
+            for (int g = 0; g < KW; ++g) {
+                if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
+                if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
+                if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+            }
+            if (wv == P - 1) {
+                const int t = 3 * b + S;
+                const int y = s0 + t - 2 * K;
+                const bool row_ok = t >= 2 * K && y < s1;
+                store_row_masked<DW>(dst_b + (int64_t)(row_ok ? y : s0) * pitch_b, row_ok ? row_bytes : 0u, st_off,
+                                     cur);
+                if (a.slots) {
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
+                    alive += (row_ok && writer) ? c : 0u;
+                }
+            } else {
+                if (S == 0) {  // the slot of block b in ring wv+1 must be free: block b-NS consumed
+                    ok = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    if (!ok) break;
+                }
+                lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
+            }
+        }
+        if (ok && wv < P - 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows written before the flag
+            if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
+        }
+    }
+    if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
 
 // 32 x 32 bit-matrix transpose in registers: afterwards x[i] bit b = (before) x[b] bit i.
@@ -1156,11 +1491,56 @@ static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s
     return hipGetLastError();
 }
 
+template <int KW, int P>
+static hipError_t launch_band_split(bool contig, const BitsArgs &a, hipStream_t s)
+{
+    const dim3 grid(a.ngroups, (int)((a.rows + a.strip - 1) / a.strip));
+    static const int sync = [] {  // 1 = LDS flags (default), 0 = one workgroup barrier per block
+        const char *e = getenv("GOL_SPLIT_SYNC");
+        return e ? atoi(e) : 1;
+    }();
+    if (sync) {
+        if (contig)
+            hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), grid, dim3(64 * P), 0, s, a);
+        else
+            hipLaunchKernelGGL((band_pipe_kernel<KW, P, false>), grid, dim3(64 * P), 0, s, a);
+    } else {
+        if (contig)
+            hipLaunchKernelGGL((band_split_kernel<KW, P, true>), grid, dim3(64 * P), 0, s, a);
+        else
+            hipLaunchKernelGGL((band_split_kernel<KW, P, false>), grid, dim3(64 * P), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+// Split-pipeline band step (k = 4 * waves per workgroup, 4 words per lane): 0 = off.
+int golk_band_split_enabled()
+{
+    static int on = [] {
+        const char *e = getenv("GOL_BAND_SPLIT");
+        return e ? atoi(e) : GOL_BAND_SPLIT_DEFAULT;
+    }();
+    return on;
+}
+
 hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
                           uint64_t *slots, hipStream_t s)
 {
     if (rows <= 0) return hipSuccess;
+    if (dw == 4 && (k == 12 || (golk_band_split_enabled() && (k == 8 || k == 16)))) {
+        BitsArgs a;
+        a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
+        a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
+        const int U = band_useful_words(k, 4);
+        a.ngroups = (int)((Wd + U - 1) / U);
+        a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
+        a.slots = slots;
+        const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
+        if (k == 8) return launch_band_split<GOL_SPLIT_KW == 4 ? 4 : 2, GOL_SPLIT_KW == 4 ? 2 : 4>(contig, a, s);
+        if (k == 12) return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s);
+        return launch_band_split<4, 4>(contig, a, s);
+    }
     BitsArgs a;
     a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
     a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;

@@ -28,7 +28,7 @@ import torch.distributed as dist
 from ._lib import GOL_COUNT_SLOTS, check, lib
 from .engine import partition_rows
 
-VALID_K = (16, 8, 4, 2, 1)
+VALID_K = (16, 12, 8, 4, 2, 1)
 
 
 class HipKernels:
@@ -120,7 +120,9 @@ class ShardedBoard:
         if layout == "band" and not self.use_band:
             raise ValueError("these kernels have no band-layout step")
         kcap = self.kern.band_max_k() if self.use_band and hasattr(self.kern, "band_max_k") else (8 if self.use_band else 16)
-        self.kmax = max(k for k in VALID_K if k <= max(1, min(turns_per_launch, min_rows, kcap)))
+        # k = 12 exists only as the band layout's split pipeline (4 words per lane)
+        self.valid_k = tuple(k for k in VALID_K if k != 12 or kcap == 12)
+        self.kmax = max(k for k in self.valid_k if k <= max(1, min(turns_per_launch, min_rows, kcap)))
         self.band = False  # buf[cur] holds the band layout
         self.kern.Wd = self.Wd
         z = dict(dtype=torch.int32, device=self.device)
@@ -217,7 +219,7 @@ class ShardedBoard:
         if turns > 0 and self.use_band:
             self._convert(True)
         while turns > 0:
-            k = max(kk for kk in VALID_K if kk <= min(self.kmax, turns))
+            k = max(kk for kk in self.valid_k if kk <= min(self.kmax, turns))
             last = turns == k
             slots = self.slots if (count and last) else None
             if slots is not None:

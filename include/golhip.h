@@ -180,8 +180,8 @@ int gol_dev_bytes_step_k(const uint8_t *top, const uint8_t *mid, const uint8_t *
 
 /* k turns of a BAND-layout bit board (bit b of word w = cell b*Wd + w); row
  * addressing and count_slots as gol_dev_bits_step.  cells_per_lane: 64 or 128
- * (2 or 4 words per lane; 0 = library default); k in {1, 2, 4, 8}, and 16 with
- * 64 cells per lane; Wd and pitch multiples of the words per lane, rows aligned
+ * (2 or 4 words per lane; 0 = library default); k in {1, 2, 4, 8}, 16 with 64
+ * cells per lane, 12 with 128 (the split pipeline: 4 waves x 3 turns); Wd and pitch multiples of the words per lane, rows aligned
  * to 4 bytes x words per lane.  Same cells as gol_dev_bits_step on the standard
  * layout, with no bit shifts in the generation. */
 int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,

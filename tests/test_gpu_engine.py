@@ -140,7 +140,8 @@ def test_kernel_variants_vs_bit_oracle(golhip, k, cpl):
         assert np.array_equal(e.store_bytes(), O.unpack(ref))
 
 
-@pytest.mark.parametrize("k,cpl", [(1, 128), (2, 128), (4, 128), (8, 128), (1, 64), (4, 64), (8, 64), (16, 64)])
+@pytest.mark.parametrize("k,cpl", [(1, 128), (2, 128), (4, 128), (8, 128), (12, 128), (1, 64), (4, 64), (8, 64),
+                                   (16, 64)])
 @pytest.mark.parametrize("shape", [(300, 1024), (97, 2048), (64, 3072), (33, 8192), (5, 1024)])
 def test_band_layout_vs_bit_oracle(golhip, k, cpl, shape):
     """Band-layout kernel (bit b of word w = cell b*W/32 + w) for every (k, words per lane):
@@ -154,6 +155,8 @@ def test_band_layout_vs_bit_oracle(golhip, k, cpl, shape):
         info = e.info()
         assert info["layout"] == "band" and info["cells_per_lane"] == cpl
         assert info["turns_per_launch"] == min(k, 16 if H >= 16 else 4 if H >= 4 else 1)
+        if k == 12:
+            assert info["turns_per_launch"] in (12, 4)  # the split pipeline (4 waves x 3 turns)
         e.step(20)
         assert e.alive_count() == counts[19]  # popcount on the band layout
         e.step(25)
@@ -332,7 +335,7 @@ def test_bench_size_k_and_shard_invariance(golhip):
     from golhip.sharded import ShardedBoard
     H, W, turns = 1 << 17, 1 << 20, 16
     hashes = []
-    for layout, k in (("standard", 1), ("standard", 8), ("standard", 16), ("band", 1), ("band", 8)):
+    for layout, k in (("standard", 1), ("standard", 8), ("standard", 16), ("band", 1), ("band", 8), ("band", 12)):
         b = ShardedBoard(H, W, turns_per_launch=k, layout=layout)
         assert b.use_band == (layout == "band")
         b.load_random(1)

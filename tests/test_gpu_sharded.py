@@ -46,7 +46,8 @@ def _worker(rank, world, port, H, W, k, turns, q, layout="auto"):
 @pytest.mark.parametrize("world,H,W,k,turns", [(2, 1024, 64 * 40, 8, 37), (3, 1000, 64 * 40, 16, 50),
                                                 (4, 515, 64 * 40, 4, 21),
                                                 # W % 1024 == 0: band layout, halos are band rows
-                                                (2, 1024, 2048, 8, 37), (3, 301, 3072, 4, 22)])
+                                                (2, 1024, 2048, 8, 37), (3, 301, 3072, 4, 22),
+                                                (2, 200, 4096, 12, 41)])
 def test_sharded_gpu_ranks_match_oracle(world, H, W, k, turns):
     import torch
     import torch.multiprocessing as mp
