@@ -752,6 +752,15 @@ __device__ __forceinline__ v4u32 lds_rd128(const lds_u32 *p)
     asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(p) : "memory");
     return r;
 }
+// Split issue / wait: the wait takes the value as an in-out operand, so every use of it is
+// ordered after the wait.
+__device__ __forceinline__ v4u32 lds_rd128_issue(const lds_u32 *p)
+{
+    v4u32 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_wait(v4u32 &r) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r)::"memory"); }
 __device__ __forceinline__ void lds_wr128(lds_u32 *p, v4u32 v)
 {
     asm volatile("ds_write_b128 %0, %1" ::"v"(p), "v"(v) : "memory");
@@ -850,11 +859,14 @@ band_pipe_kernel(BitsArgs a)
             ok = spin_until_ge(ready_l + wv, b + 1);
             if (!ok) break;
         }
+        v4u32 nextv = lds_rd128_issue(slot_row(wv, b, 0));
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[DW];
             {
-                const v4u32 v = lds_rd128(slot_row(wv, b, S));  // waited: block b row S is in VGPRs
+                v4u32 v = nextv;
+                lds_wait(v);  // block b row S is in VGPRs; row S+1 is read while row S computes
+                if (S < 2) nextv = lds_rd128_issue(slot_row(wv, b, S + 1));
                 cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
             }
             if (S == 2) {
