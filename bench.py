@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="weak", choices=["weak", "bit64k", "byte16k"])
     ap.add_argument("--k", type=int, default=0,
-                    help="turns per launch (temporal blocking); 0 = 8 for bit boards, 16 for byte16k")
+                    help="turns per launch (temporal blocking); 0 = library default for bit boards "
+                         "(12 band / 8 standard), 16 for byte16k")
     ap.add_argument("--cpl", type=int, default=0, help="cells per lane (32/64/128; 0 = library default)")
     ap.add_argument("--strip", type=int, default=0, help="rows per wave strip (0 = auto)")
     ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"],
@@ -264,8 +265,8 @@ def run_bytes(args, rank, world):
 
 def main():
     args = parse()
-    if args.k <= 0:
-        args.k = 16 if args.workload == "byte16k" else 8
+    if args.k <= 0 and args.workload == "byte16k":
+        args.k = 16  # bit boards: 0 = library default (12 on the band layout, 8 on the standard one)
     rank, world, local = setup(args)
     if args.workload == "byte16k":
         value, dt, cfg, roof, dtype = run_bytes(args, rank, world)

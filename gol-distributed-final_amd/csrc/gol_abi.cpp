@@ -176,7 +176,7 @@ extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, go
         if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     }
     e->device = dev;
-    e->k = (cfg && cfg->turns_per_launch > 0) ? cfg->turns_per_launch : GOL_DEFAULT_K;
+    e->k = (cfg && cfg->turns_per_launch > 0) ? cfg->turns_per_launch : 0;  // 0: per layout, below
     int cpl = (cfg && cfg->cells_per_lane > 0) ? cfg->cells_per_lane : 32 * GOL_DEFAULT_DW;
     if (cpl != 32 && cpl != 64 && cpl != 128) {
         delete e;
@@ -197,6 +197,7 @@ extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, go
         return gol_set_error(GOL_EINVAL, "the band layout needs W %% 1024 == 0");
     }
     e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
+    if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
     int rc = engine_dev(e);
     if (rc == GOL_OK) {
         hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);

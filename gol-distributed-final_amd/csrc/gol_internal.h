@@ -9,7 +9,10 @@
 // Library defaults for the bit-board step (chosen from the gfx950 sweep recorded
 // in DESIGN.md; overridable per engine through gol_config).
 #ifndef GOL_DEFAULT_K
-#define GOL_DEFAULT_K 8
+#define GOL_DEFAULT_K 8        // standard layout
+#endif
+#ifndef GOL_DEFAULT_BAND_K
+#define GOL_DEFAULT_BAND_K 12  // band layout, 4 words per lane: the split pipeline
 #endif
 #ifndef GOL_DEFAULT_DW
 #define GOL_DEFAULT_DW 2

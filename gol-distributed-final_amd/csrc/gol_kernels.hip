@@ -1546,7 +1546,9 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
         a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
         const int U = band_useful_words(k, 4);
         a.ngroups = (int)((Wd + U - 1) / U);
-        a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
+        // one workgroup per (column group, strip): strips up to 1024 rows (measured best at k = 12)
+        a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP)
+                            : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(1024, rows * a.ngroups / 2048)));
         a.slots = slots;
         const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
         if (k == 8) return launch_band_split<GOL_SPLIT_KW == 4 ? 4 : 2, GOL_SPLIT_KW == 4 ? 2 : 4>(contig, a, s);

@@ -90,7 +90,7 @@ class HipKernels:
 class ShardedBoard:
     """A W-wide, H-tall bit-packed torus, rows sharded over the ranks of `group`."""
 
-    def __init__(self, height: int, width: int, *, turns_per_launch: int = 8, cells_per_lane: int = 0,
+    def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
                  strip_rows: int = 0, device=None, kernels=None, group=None, layout: str = "auto"):
         if width % 64:
             raise ValueError("the sharded bit board needs W % 64 == 0")
@@ -122,6 +122,8 @@ class ShardedBoard:
         kcap = self.kern.band_max_k() if self.use_band and hasattr(self.kern, "band_max_k") else (8 if self.use_band else 16)
         # k = 12 exists only as the band layout's split pipeline (4 words per lane)
         self.valid_k = tuple(k for k in VALID_K if k != 12 or kcap == 12)
+        if turns_per_launch <= 0:  # library defaults: 12 on the band layout (split pipeline), else 8
+            turns_per_launch = 12 if (self.use_band and kcap == 12) else 8
         self.kmax = max(k for k in self.valid_k if k <= max(1, min(turns_per_launch, min_rows, kcap)))
         self.band = False  # buf[cur] holds the band layout
         self.kern.Wd = self.Wd
