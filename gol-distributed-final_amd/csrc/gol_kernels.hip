@@ -772,13 +772,16 @@ __device__ __forceinline__ int lds_rd32(const lds_u32 *p)
     return r;
 }
 __device__ __forceinline__ void lds_wr32(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
-__device__ __forceinline__ bool spin_until_ge(const lds_u32 *f, int v)
+// Wait until flag f >= v; returns the value seen (callers cache it: a producer is usually
+// several blocks ahead, so most blocks need no flag read), or -1 after the spin bound.
+__device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 {
     for (int n = 0; n < (1 << 22); ++n) {
-        if (__builtin_amdgcn_readfirstlane(lds_rd32(f)) >= v) return true;
+        const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
+        if (x >= v) return x;
         __builtin_amdgcn_s_sleep(1);
     }
-    return false;
+    return -1;
 }
 
 template <int KW, int P, bool CONTIG>
@@ -849,14 +852,20 @@ band_pipe_kernel(BitsArgs a)
         if (nblk > 1) stage_in(1, ring[0][1 % NS]);
     }
     uint32_t alive = 0;
+    const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
     bool ok = true;
+    int seen_ready = 0, seen_free = 0;  // cached flag values (ring wv ready, ring wv+1 consumed)
+    // last wave: row y = s0 + 3b + S - 2K is stored iff 0 <= 3b + S - 2K < s1 - s0
+    const uint32_t nrows = (uint32_t)(s1 - s0);
+    char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch_b;  // row of (b, S) = (0, 0), advanced per row
     for (int b = 0; b < nblk && ok; ++b) {
         // input block b
         if (wv == 0) {
             if (b + 1 < nblk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // block b+1 may stay in flight
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            ok = spin_until_ge(ready_l + wv, b + 1);
+        } else if (seen_ready < b + 1) {
+            seen_ready = spin_until_ge(ready_l + wv, b + 1);
+            ok = seen_ready >= 0;
             if (!ok) break;
         }
         v4u32 nextv = lds_rd128_issue(slot_row(wv, b, 0));
@@ -887,20 +896,19 @@ band_pipe_kernel(BitsArgs a)
                 if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
             }
             if (wv == P - 1) {
-                const int t = 3 * b + S;
-                const int y = s0 + t - 2 * K;
-                const bool row_ok = t >= 2 * K && y < s1;
-                store_row_masked<DW>(dst_b + (int64_t)(row_ok ? y : s0) * pitch_b, row_ok ? row_bytes : 0u, st_off,
-                                     cur);
+                const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
+                store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
+                srow += pitch_b;
                 if (a.slots) {
                     uint32_t c = 0;
 #pragma unroll
                     for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
-                    alive += (row_ok && writer) ? c : 0u;
+                    alive += bitop3<0x80>(c, st_mask, row_ok ? 0xFFFFFFFFu : 0u);  // c & writer & row_ok
                 }
             } else {
-                if (S == 0) {  // the slot of block b in ring wv+1 must be free: block b-NS consumed
-                    ok = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                if (S == 0 && seen_free < b + 1 - NS) {  // slot b % NS of ring wv+1 free: block b-NS consumed
+                    seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    ok = seen_free >= 0;
                     if (!ok) break;
                 }
                 lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
