@@ -12,19 +12,18 @@ from ._lib import GOL_EFORMAT, GolError
 _SPACE = b" \t\n\v\f\r"
 
 
-def read_pgm(path: str, width: int | None = None, height: int | None = None) -> np.ndarray:
-    """io.go:90-126: fields = strings.Fields(data); "P5", width, height, 255, pixels."""
-    with open(path, "rb") as f:
-        data = f.read()
-    fields, i, n = [], 0, len(data)
+def pgm_header(head: bytes, width: int | None = None, height: int | None = None) -> tuple[int, int, int]:
+    """io.go:90-126 header rules on the first bytes of a P5 file: fields = strings.Fields(data);
+    "P5", width, height, 255.  Returns (W, H, offset of the first raster byte)."""
+    fields, i, n = [], 0, len(head)
     while i < n and len(fields) < 4:
-        while i < n and data[i] in _SPACE:
+        while i < n and head[i] in _SPACE:
             i += 1
         j = i
-        while j < n and data[j] not in _SPACE:
+        while j < n and head[j] not in _SPACE:
             j += 1
         if j > i:
-            fields.append(data[i:j])
+            fields.append(head[i:j])
         i = j
     if not fields or fields[0] != b"P5":
         raise GolError(GOL_EFORMAT, "Not a pgm file")
@@ -38,11 +37,32 @@ def read_pgm(path: str, width: int | None = None, height: int | None = None) -> 
         raise GolError(GOL_EFORMAT, "Incorrect height")
     if maxval != 255:
         raise GolError(GOL_EFORMAT, "Incorrect maxval/bit depth")
-    # one whitespace byte separates maxval from the raster
-    pix = np.frombuffer(data, dtype=np.uint8, count=W * H, offset=i + 1) if n >= i + 1 + W * H else None
-    if pix is None:
+    return W, H, i + 1  # one whitespace byte separates maxval from the raster
+
+
+def read_pgm(path: str, width: int | None = None, height: int | None = None) -> np.ndarray:
+    """io.go:90-126 readPgmImage: the whole raster as an (H, W) uint8 array."""
+    with open(path, "rb") as f:
+        data = f.read()
+    W, H, off = pgm_header(data[:4096], width, height)
+    if len(data) < off + W * H:
         raise GolError(GOL_EFORMAT, "pixel data shorter than W*H")
-    return pix.reshape(H, W).copy()
+    return np.frombuffer(data, dtype=np.uint8, count=W * H, offset=off).reshape(H, W).copy()
+
+
+def pgm_rows(path: str, y0: int, y1: int, width: int | None = None, height: int | None = None):
+    """Rows [y0, y1) of a P5 file as a read-only (y1-y0, W) memory map: a rank of a sharded
+    board reads only its own rows (a 2^20 x 2^20 image is 1 TiB)."""
+    with open(path, "rb") as f:
+        head = f.read(4096)
+        f.seek(0, 2)
+        size = f.tell()
+    W, H, off = pgm_header(head, width, height)
+    if size < off + W * H:
+        raise GolError(GOL_EFORMAT, "pixel data shorter than W*H")
+    if not 0 <= y0 <= y1 <= H:
+        raise ValueError(f"rows [{y0}, {y1}) outside the {H}-row image")
+    return np.memmap(path, dtype=np.uint8, mode="r", offset=off + y0 * W, shape=(y1 - y0, W))
 
 
 def write_pgm_bytes(board: np.ndarray) -> bytes:

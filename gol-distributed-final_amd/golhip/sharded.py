@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -81,10 +82,11 @@ class HipKernels:
         check(lib().gol_dev_unpack(src.data_ptr(), rows, W, pitch, out.data_ptr(), W, self._stream()))
         return out
 
-    def pack(self, board, dst) -> None:
+    def pack(self, board, dst, nonbinary=None) -> None:
+        """0/255 bytes -> bits; nonbinary (int32 device tensor) gets 1 if any byte is neither."""
         rows, W = board.shape
-        check(lib().gol_dev_pack(board.data_ptr(), rows, W, W, dst.data_ptr(), dst.shape[1], None,
-                                 self._stream()))
+        check(lib().gol_dev_pack(board.data_ptr(), rows, W, W, dst.data_ptr(), dst.shape[1],
+                                 nonbinary.data_ptr() if nonbinary is not None else None, self._stream()))
 
 
 class ShardedBoard:
@@ -169,6 +171,23 @@ class ShardedBoard:
         if tuple(board_rows.shape) != (self.R, self.W):
             raise ValueError("expected this rank's (R, W) rows")
         self.kern.pack(board_rows.to(self.device).contiguous(), self.board)
+        self.band = False
+        self.turn = 0
+
+    def load_pgm(self, path: str, chunk_rows: int = 4096) -> None:
+        """Stream this rank's rows [y0, y1) of a P5 image (gol/io.go:90-126 header rules) into
+        the shard: memory-mapped row chunks -> device -> packed, so no rank holds more than one
+        chunk of bytes.  The reference's images are 0/255; other bytes need the exact first
+        turn of the single-GPU engine (worker.go:26-37) and are rejected here."""
+        from .pgm import pgm_rows
+        rows = pgm_rows(path, self.y0, self.y1, self.W, self.H)
+        flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        for a in range(0, self.R, chunk_rows):
+            n = min(chunk_rows, self.R - a)
+            chunk = torch.from_numpy(np.ascontiguousarray(rows[a:a + n])).to(self.device)
+            self.kern.pack(chunk, self.board[a:a + n], flag)
+        if int(flag.item()):
+            raise ValueError(f"{path}: bytes other than 0/255 (use the single-GPU engine for those)")
         self.band = False
         self.turn = 0
 

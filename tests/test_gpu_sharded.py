@@ -7,6 +7,7 @@ shards and the interior/boundary launch split -- and equals the single-rank resu
 import os
 import socket
 
+import numpy as np
 import pytest
 
 from oracle import oracle as O
@@ -67,3 +68,67 @@ def test_sharded_gpu_ranks_match_oracle(world, H, W, k, turns):
     for rank, h, count, fused in res:
         assert h == O.hash_words(ref)
         assert count == fused == O.popcount_words(ref)
+
+
+def _pgm_worker(rank, world, port, path, W, H, turns, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "gol-distributed-final_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from golhip.sharded import ShardedBoard
+        b = ShardedBoard(H, W)
+        b.load_pgm(path, chunk_rows=100)
+        b.step(turns, count=True)
+        torch.cuda.synchronize()
+        full = b.gather_bytes()
+        q.put((rank, b.fused_count(), full.numpy() if full is not None else None))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_pgm(world, path, W, H, turns):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pgm_worker, args=(r, world, port, path, W, H, turns, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (c, full) for r, c, full in (q.get(timeout=150) for _ in range(world))}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_sharded_gpu_load_pgm_golden(golden_dir):
+    """Two ranks stream their rows of images/512x512.pgm into GPU shards; after 100 turns the
+    gathered board is check/images/512x512x100.pgm."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_pgm(2, os.path.join(golden_dir, "images", "512x512.pgm"), 512, 512, 100)
+    _, _, want = O.read_pgm(os.path.join(golden_dir, "check", "images", "512x512x100.pgm"))
+    assert np.array_equal(res[0][1], want)
+    assert res[0][0] == res[1][0] == int(np.count_nonzero(want))
+
+
+def test_sharded_gpu_load_pgm_band(tmp_path):
+    """A 2048-wide PGM (band layout, k = 12 split pipeline) streamed into 3 shards."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    H, W, turns = 150, 2048, 29
+    rng = np.random.default_rng(5)
+    board = (rng.random((H, W)) < 0.4).astype(np.uint8) * 255
+    p = tmp_path / "b.pgm"
+    p.write_bytes(O.pgm_bytes(board))
+    res = _run_pgm(3, str(p), W, H, turns)
+    ref = O.unpack(O.bits_run(O.pack(board), turns))
+    assert np.array_equal(res[0][1], ref)

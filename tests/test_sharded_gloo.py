@@ -82,8 +82,11 @@ class OracleKernels:
         w = np.ascontiguousarray(src.numpy().view(np.uint32)[:, :self.Wd]).view(np.uint64)
         return torch.from_numpy(O.unpack(w))
 
-    def pack(self, board, dst):
-        dst.numpy().view(np.uint32)[:, :self.Wd] = O.pack(board.numpy()).view(np.uint32)
+    def pack(self, board, dst, nonbinary=None):
+        b = board.numpy()
+        dst.numpy().view(np.uint32)[:, :self.Wd] = O.pack(b).view(np.uint32)
+        if nonbinary is not None and ((b != 0) & (b != 255)).any():
+            nonbinary[0] = 1
 
 
 def _free_port():
@@ -148,3 +151,58 @@ def test_sharded_matches_oracle(world, H, W, k, turns):
     assert np.array_equal(res[0][-2], O.unpack(ref))
     import hashlib
     assert res[0][-1] == hashlib.sha256(O.pgm_bytes(O.unpack(ref))).hexdigest()  # gol/io.go P5 bytes
+
+
+def _pgm_worker(rank, world, port, path, W, H, turns, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from golhip.sharded import ShardedBoard
+        b = ShardedBoard(H, W, turns_per_launch=8, kernels=OracleKernels(), device="cpu")
+        b.load_pgm(path, chunk_rows=7)  # odd chunks: several per shard
+        b.step(turns)
+        full = b.gather_bytes()
+        q.put((rank, full.numpy() if full is not None else None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_load_pgm_golden(world, golden_dir):
+    """Each rank streams only its rows of images/512x512.pgm (memory-mapped, gol/io.go header
+    rules); 100 turns on the sharded board reproduce check/images/512x512x100.pgm."""
+    path = os.path.join(golden_dir, "images", "512x512.pgm")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pgm_worker, args=(r, world, port, path, 512, 512, 100, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    _, _, want = O.read_pgm(os.path.join(golden_dir, "check", "images", "512x512x100.pgm"))
+    assert np.array_equal(res[0], want)
+
+
+def test_pgm_rows_header_rules(tmp_path):
+    """golhip.pgm.pgm_rows: header rules of gol/io.go:98-119 and row windows of the raster."""
+    from golhip._lib import GolError
+    from golhip.pgm import pgm_rows
+    board = (np.arange(6 * 8).reshape(6, 8) % 2 * 255).astype(np.uint8)
+    p = tmp_path / "b.pgm"
+    p.write_bytes(O.pgm_bytes(board))
+    assert np.array_equal(np.asarray(pgm_rows(str(p), 2, 5)), board[2:5])
+    assert np.array_equal(np.asarray(pgm_rows(str(p), 0, 6, 8, 6)), board)
+    with pytest.raises(GolError):
+        pgm_rows(str(p), 0, 1, width=9)
+    bad = tmp_path / "bad.pgm"
+    bad.write_bytes(b"P6\n8 6\n255\n" + board.tobytes())
+    with pytest.raises(GolError):
+        pgm_rows(str(bad), 0, 1)
+    short = tmp_path / "short.pgm"
+    short.write_bytes(O.pgm_bytes(board)[:-3])
+    with pytest.raises(GolError):
+        pgm_rows(str(short), 0, 1)
