@@ -737,6 +737,19 @@ band_split_kernel(BitsArgs a)
 // consumer has taken block b - NS; a consumer may read block b once ready > b.  The chain
 // has no cycle, and every spin is bounded (a protocol fault ends the wave, and the parity
 // tests then fail, instead of hanging the GPU).
+#ifndef GOL_PIPE_ROTATE
+#define GOL_PIPE_ROTATE 1  // rotate pipeline roles over the SIMDs by workgroup
+#endif
+#ifndef GOL_PIPE_ABL
+#define GOL_PIPE_ABL 0  // measurement only (wrong results): 1 = no flag waits, 2 = no LDS row traffic,
+                        // 4 = no HBM traffic, 8 = no stores, 16 = no input loads
+#endif
+#ifndef GOL_SPIN_SLEEP
+#define GOL_SPIN_SLEEP 1  // s_sleep argument between flag polls (units of 64 cycles)
+#endif
+#ifndef GOL_PIPE_IN_SLOTS
+#define GOL_PIPE_IN_SLOTS 3  // input ring slots (staging runs NSI-1 blocks ahead; 4 and 5 measured no faster)
+#endif
 #ifndef GOL_PIPE_SLOTS
 #define GOL_PIPE_SLOTS 3
 #endif
@@ -779,7 +792,7 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
     for (int n = 0; n < (1 << 22); ++n) {
         const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
         if (x >= v) return x;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
     }
     return -1;
 }
@@ -794,11 +807,16 @@ band_pipe_kernel(BitsArgs a)
     constexpr int U = band_useful_words(K, DW);
     constexpr int ROW = 64 * DW;
     constexpr int NS = GOL_PIPE_SLOTS;
-    __shared__ uint32_t ring[P][NS][3][ROW];
+    constexpr int NSI = GOL_PIPE_IN_SLOTS;  // input ring: blocks b .. b+NSI-2 in flight
+    __shared__ uint32_t in_ring[NSI][3][ROW];
+    __shared__ uint32_t ring[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
     __shared__ int ready[P], consumed[P];
 
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // Pipeline position of this wave.  Rotated by workgroup: the waves of a workgroup sit on
+    // the CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put
+    // its loader (global_load_lds) on one SIMD and its storer on another.
+    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + GOL_PIPE_ROTATE * (blockIdx.x + blockIdx.y)) % P);
     const int group = blockIdx.x;
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
@@ -824,7 +842,7 @@ band_pipe_kernel(BitsArgs a)
     const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
 
-    // wave 0: block b -> ring[0][b % NS] (global_load_lds).  The slot is an argument: a lambda
+    // wave 0: block b -> in_ring[b % NSI] (global_load_lds).  The slot is an argument: a lambda
     // that captures a __shared__ array silently loses the kernel's host-side stub.
     auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
 #pragma unroll
@@ -840,20 +858,26 @@ band_pipe_kernel(BitsArgs a)
     if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
     __syncthreads();
     lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
+    lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
     constexpr int SLOT = 3 * ROW;  // uint32 per slot (one block)
-    auto slot_row = [&](int e, int b, int S) { return ring_l + (e * NS + b % NS) * SLOT + S * ROW + lane * 4; };
+    auto slot_row = [&](int e, int b, int S) {
+        return e == 0 ? in_l + (b % NSI) * SLOT + S * ROW + lane * 4
+                      : ring_l + ((e - 1) * NS + b % NS) * SLOT + S * ROW + lane * 4;
+    };
 
     Pipe<KW, DW> p;
     PipeSel<KW, DW, 0>::init(p);
     if (wv == 0) {
-        stage_in(0, ring[0][0]);
-        if (nblk > 1) stage_in(1, ring[0][1 % NS]);
+#pragma unroll
+        for (int i = 0; i < NSI - 1; ++i)
+            if (i < nblk) stage_in(i, in_ring[i]);
     }
     uint32_t alive = 0;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
     bool ok = true;
+    v4u32 fake = v4u32{(uint32_t)lane, 7u, (uint32_t)blockIdx.x, 9u};  // GOL_PIPE_ABL & 2 only
     int seen_ready = 0, seen_free = 0;  // cached flag values (ring wv ready, ring wv+1 consumed)
     // last wave: row y = s0 + 3b + S - 2K is stored iff 0 <= 3b + S - 2K < s1 - s0
     const uint32_t nrows = (uint32_t)(s1 - s0);
@@ -861,26 +885,31 @@ band_pipe_kernel(BitsArgs a)
     for (int b = 0; b < nblk && ok; ++b) {
         // input block b
         if (wv == 0) {
-            if (b + 1 < nblk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // block b+1 may stay in flight
+            // block b landed; blocks b+1 .. b+NSI-2 (if any) may stay in flight
+            const int inflight = min(NSI - 2, nblk - 1 - b);
+            if (inflight >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+            else if (inflight == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if (inflight == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (seen_ready < b + 1) {
-            seen_ready = spin_until_ge(ready_l + wv, b + 1);
+            seen_ready = (GOL_PIPE_ABL & 1) ? b + 1 : spin_until_ge(ready_l + wv, b + 1);
             ok = seen_ready >= 0;
             if (!ok) break;
         }
-        v4u32 nextv = lds_rd128_issue(slot_row(wv, b, 0));
+        v4u32 nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, 0));
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[DW];
             {
                 v4u32 v = nextv;
-                lds_wait(v);  // block b row S is in VGPRs; row S+1 is read while row S computes
-                if (S < 2) nextv = lds_rd128_issue(slot_row(wv, b, S + 1));
+                if (!(GOL_PIPE_ABL & 2)) lds_wait(v);  // block b row S is in VGPRs; row S+1 is read while row S computes
+                if (S < 2) nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, S + 1));
                 cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
             }
             if (S == 2) {
                 if (wv == 0) {
-                    if (b + 2 < nblk) stage_in(b + 2, ring[0][(b + 2) % NS]);  // refills slot (b-1) % NS
+                    if (!(GOL_PIPE_ABL & 20) && b + NSI - 1 < nblk)
+                        stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);  // refills slot (b-1) % NSI
                 } else if (lane == 0) {
                     lds_wr32(consumed_l + wv, b + 1);
                 }
@@ -897,7 +926,7 @@ band_pipe_kernel(BitsArgs a)
             }
             if (wv == P - 1) {
                 const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
+                if (!(GOL_PIPE_ABL & 12)) store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
                 srow += pitch_b;
                 if (a.slots) {
                     uint32_t c = 0;
@@ -907,11 +936,12 @@ band_pipe_kernel(BitsArgs a)
                 }
             } else {
                 if (S == 0 && seen_free < b + 1 - NS) {  // slot b % NS of ring wv+1 free: block b-NS consumed
-                    seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    seen_free = (GOL_PIPE_ABL & 1) ? b + 1 : spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
                     ok = seen_free >= 0;
                     if (!ok) break;
                 }
-                lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
+                if (!(GOL_PIPE_ABL & 2)) lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
+                else fake = v4u32{cur[0], cur[1], cur[2], cur[3]} ^ fake;
             }
         }
         if (ok && wv < P - 1) {
