@@ -740,6 +740,9 @@ band_split_kernel(BitsArgs a)
 #ifndef GOL_PIPE_ROTATE
 #define GOL_PIPE_ROTATE 1  // rotate pipeline roles over the SIMDs by workgroup
 #endif
+#ifndef GOL_PIPE_PROFILE
+#define GOL_PIPE_PROFILE 0  // diagnostic build: per-role wait-cycle sums instead of the alive count
+#endif
 #ifndef GOL_PIPE_ABL
 #define GOL_PIPE_ABL 0  // measurement only (wrong results): 1 = no flag waits, 2 = no LDS row traffic,
                         // 4 = no HBM traffic, 8 = no stores, 16 = no input loads
@@ -882,8 +885,18 @@ band_pipe_kernel(BitsArgs a)
     // last wave: row y = s0 + 3b + S - 2K is stored iff 0 <= 3b + S - 2K < s1 - s0
     const uint32_t nrows = (uint32_t)(s1 - s0);
     char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch_b;  // row of (b, S) = (0, 0), advanced per row
+#if GOL_PIPE_PROFILE
+    uint64_t pt_in = 0, pt_free = 0, pt_lds = 0, pt_mark;
+    const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#define PT_BEGIN() pt_mark = __builtin_amdgcn_s_memtime()
+#define PT_END(acc) acc += __builtin_amdgcn_s_memtime() - pt_mark
+#else
+#define PT_BEGIN()
+#define PT_END(acc)
+#endif
     for (int b = 0; b < nblk && ok; ++b) {
         // input block b
+        PT_BEGIN();
         if (wv == 0) {
             // block b landed; blocks b+1 .. b+NSI-2 (if any) may stay in flight
             const int inflight = min(NSI - 2, nblk - 1 - b);
@@ -896,13 +909,16 @@ band_pipe_kernel(BitsArgs a)
             ok = seen_ready >= 0;
             if (!ok) break;
         }
+        PT_END(pt_in);
         v4u32 nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, 0));
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[DW];
             {
                 v4u32 v = nextv;
+                PT_BEGIN();
                 if (!(GOL_PIPE_ABL & 2)) lds_wait(v);  // block b row S is in VGPRs; row S+1 is read while row S computes
+                PT_END(pt_lds);
                 if (S < 2) nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, S + 1));
                 cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
             }
@@ -936,7 +952,9 @@ band_pipe_kernel(BitsArgs a)
                 }
             } else {
                 if (S == 0 && seen_free < b + 1 - NS) {  // slot b % NS of ring wv+1 free: block b-NS consumed
+                    PT_BEGIN();
                     seen_free = (GOL_PIPE_ABL & 1) ? b + 1 : spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    PT_END(pt_free);
                     ok = seen_free >= 0;
                     if (!ok) break;
                 }
@@ -950,6 +968,19 @@ band_pipe_kernel(BitsArgs a)
         }
     }
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if GOL_PIPE_PROFILE
+    // diagnostic build only: per-role cycle sums in slots[role*64 + 8*i] (i: total, input wait,
+    // free-slot wait, LDS row wait, waves)
+    if (lane == 0 && a.slots) {
+        unsigned long long *q = (unsigned long long *)a.slots + wv * 64;
+        atomicAdd(q + 0, (unsigned long long)(__builtin_amdgcn_s_memtime() - pt0));
+        atomicAdd(q + 8, (unsigned long long)pt_in);
+        atomicAdd(q + 16, (unsigned long long)pt_free);
+        atomicAdd(q + 24, (unsigned long long)pt_lds);
+        atomicAdd(q + 32, 1ull);
+    }
+    return;
+#endif
     if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
 
