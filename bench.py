@@ -192,11 +192,17 @@ def run_bits(args, rank, world):
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc.get("bytes_per_launch") if pmc else None,
+            # with k turns per launch the kernel is bound by VALU issue, not HBM:
+            # the PMC-measured share of the 2-cycle VALU issue peak, from the same profile
+            "valu_issue_frac": pmc.get("valu_issue_frac") if pmc else None,
             "basis": f"{BITS_BYTES_PER_UPDATE} B/cell-update x {krows}x{W} cells x {kk} turns per launch "
                      f"/ {kms:.3f} ms mean launch ({len(timer.pairs)} launches, HIP events)",
             "hbm_min_bytes_frac": round(2 * krows * W / 8 / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     del lib
-    cfg = {"workload": ("weak-2^17x2^20-per-gpu" if args.workload == "weak" else "bit-65536x65536"),
+    rpg = args.rows_per_gpu
+    rows_name = f"2^{rpg.bit_length() - 1}" if rpg & (rpg - 1) == 0 else str(rpg)
+    wname = f"2^{W.bit_length() - 1}" if W & (W - 1) == 0 else str(W)
+    cfg = {"workload": (f"weak-{rows_name}x{wname}-per-gpu" if args.workload == "weak" else "bit-65536x65536"),
            "H": H, "W": W, "parallelism": (f"rows{world}" if nshards > 1 else (f"replicas{world}" if world > 1 else "1gpu")),
            **info}
     dtype = "u32 (bit-packed, 32 cells/word" + (", column-band layout)" if layout == "band" else ")")

@@ -456,6 +456,38 @@ __device__ __forceinline__ void bstage_seq(Pipe<K, DW> &p, const int g, uint32_t
                       p.h1[g][S][j], p.cc[g][SM][j]);
 }
 
+// Vertical-first stage (band layout): per word the vertical 3-sum of the column
+// (v0, v1) = c(y-1) + c(y) + c(y+1), then the horizontal sum of the three neighbouring
+// columns' (v0, v1) and the rule with the centre cell c(y).  Same 10 bitwise ops per word
+// as bstage (the sharing moves from vertical to horizontal: 2 DPP per lane edge instead
+// of 1), but the stage state is only the last two input rows: 2 VGPRs per word instead
+// of 5 (in the standard layout the same reordering doubled the shifts; here there are none).
+template <int K, int DW>
+struct PipeV {
+    uint32_t c[K][3][DW];
+};
+
+template <int K, int DW, int S>
+__device__ __forceinline__ void vstage(PipeV<K, DW> &p, const int g, uint32_t (&cur)[DW])
+{
+    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
+    uint32_t v0[DW], v1[DW];
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+        p.c[g][S][j] = cur[j];
+        v0[j] = bitop3<TT_XOR3>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
+        v1[j] = bitop3<TT_MAJ>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
+    }
+    const uint32_t l0 = from_lower_lane(v0[DW - 1]), l1 = from_lower_lane(v1[DW - 1]);
+    const uint32_t r0 = from_upper_lane(v0[0]), r1 = from_upper_lane(v1[0]);
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+        const uint32_t a0 = j == 0 ? l0 : v0[j - 1], a1 = j == 0 ? l1 : v1[j - 1];
+        const uint32_t c0 = j == DW - 1 ? r0 : v0[j + 1], c1 = j == DW - 1 ? r1 : v1[j + 1];
+        cur[j] = rule(a0, a1, v0[j], v1[j], c0, c1, p.c[g][SM][j]);
+    }
+}
+
 __host__ __device__ constexpr int band_halo_lanes(int k, int dw) { return (k + dw - 1) / dw; }
 __host__ __device__ constexpr int band_useful_words(int k, int dw) { return (64 - 2 * band_halo_lanes(k, dw)) * dw; }
 
@@ -476,7 +508,7 @@ __host__ __device__ constexpr int band_useful_words(int k, int dw) { return (64 
 // of 4 waves along the row, grid.y: strips of output rows.  A lane holds DW words.
 // CONTIG: top == mid - K*pitch and bot == mid + R*pitch (halo rows stored right above and
 // below the shard), so input row y is simply mid + y*pitch: no per-row segment select.
-template <int K, int DW, bool CONTIG>
+template <int K, int DW, bool CONTIG, bool VF = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_BAND_MIN_WAVES, 8)))
 band_step_kernel(BitsArgs a)
 {
@@ -534,8 +566,17 @@ band_step_kernel(BitsArgs a)
         }
     };
 
-    Pipe<K, DW> p;
-    PipeSel<K, DW, 0>::init(p);
+    typename std::conditional<VF, PipeV<K, DW>, Pipe<K, DW>>::type p;
+    if constexpr (VF) {
+#pragma unroll
+        for (int g = 0; g < K; ++g)
+#pragma unroll
+            for (int s2 = 0; s2 < 3; ++s2)
+#pragma unroll
+                for (int j = 0; j < DW; ++j) p.c[g][s2][j] = 0;
+    } else {
+        PipeSel<K, DW, 0>::init(p);
+    }
 
     // Row blocks in flight: a ring of PF+1 three-row buffers; block b lives in ring[b % (PF+1)]
     // and is loaded PF blocks ahead of use.  The block loop is unrolled by PF+1 so the ring
@@ -566,9 +607,15 @@ band_step_kernel(BitsArgs a)
             for (int s = 0; s < 3; ++s) unwrap(cur[s]);
 #pragma unroll
             for (int w = 0; w < K + 2; ++w) {
-                if (w < K) bstage<K, DW, 0>(p, w, cur[0]);
-                if (w >= 1 && w - 1 < K) bstage<K, DW, 1>(p, w - 1, cur[1]);
-                if (w >= 2 && w - 2 < K) bstage<K, DW, 2>(p, w - 2, cur[2]);
+                if constexpr (VF) {
+                    if (w < K) vstage<K, DW, 0>(p, w, cur[0]);
+                    if (w >= 1 && w - 1 < K) vstage<K, DW, 1>(p, w - 1, cur[1]);
+                    if (w >= 2 && w - 2 < K) vstage<K, DW, 2>(p, w - 2, cur[2]);
+                } else {
+                    if (w < K) bstage<K, DW, 0>(p, w, cur[0]);
+                    if (w >= 1 && w - 1 < K) bstage<K, DW, 1>(p, w - 1, cur[1]);
+                    if (w >= 2 && w - 2 < K) bstage<K, DW, 2>(p, w - 2, cur[2]);
+                }
             }
 #pragma unroll
             for (int S = 0; S < 3; ++S) {
@@ -737,6 +784,15 @@ band_split_kernel(BitsArgs a)
 // consumer has taken block b - NS; a consumer may read block b once ready > b.  The chain
 // has no cycle, and every spin is bounded (a protocol fault ends the wave, and the parity
 // tests then fail, instead of hanging the GPU).
+#ifndef GOL_BAND_VF_DEFAULT
+#define GOL_BAND_VF_DEFAULT 0  // 1: band k = 8/12/16 with 4 words per lane on the vertical-first kernel
+#endif
+#ifndef GOL_PIPE_VF_DEFAULT
+#define GOL_PIPE_VF_DEFAULT 0  // 1: k = 12 as GOL_PIPE_VF_P waves of vertical-first stages
+#endif
+#ifndef GOL_PIPE_VF_P
+#define GOL_PIPE_VF_P 2
+#endif
 #ifndef GOL_PIPE_ROTATE
 #define GOL_PIPE_ROTATE 1  // rotate pipeline roles over the SIMDs by workgroup
 #endif
@@ -800,7 +856,7 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
     return -1;
 }
 
-template <int KW, int P, bool CONTIG>
+template <int KW, int P, bool CONTIG, bool VF = false>
 __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(GOL_SPLIT_MIN_WAVES, 8)))
 band_pipe_kernel(BitsArgs a)
 {
@@ -870,8 +926,17 @@ band_pipe_kernel(BitsArgs a)
                       : ring_l + ((e - 1) * NS + b % NS) * SLOT + S * ROW + lane * 4;
     };
 
-    Pipe<KW, DW> p;
-    PipeSel<KW, DW, 0>::init(p);
+    typename std::conditional<VF, PipeV<KW, DW>, Pipe<KW, DW>>::type p;
+    if constexpr (VF) {
+#pragma unroll
+        for (int g = 0; g < KW; ++g)
+#pragma unroll
+            for (int s2 = 0; s2 < 3; ++s2)
+#pragma unroll
+                for (int j = 0; j < DW; ++j) p.c[g][s2][j] = 0;
+    } else {
+        PipeSel<KW, DW, 0>::init(p);
+    }
     if (wv == 0) {
 #pragma unroll
         for (int i = 0; i < NSI - 1; ++i)
@@ -936,9 +1001,15 @@ band_pipe_kernel(BitsArgs a)
             }
 #pragma unroll
             for (int g = 0; g < KW; ++g) {
-                if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
-                if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
-                if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+                if constexpr (VF) {
+                    if (S == 0) vstage<KW, DW, 0>(p, g, cur);
+                    if (S == 1) vstage<KW, DW, 1>(p, g, cur);
+                    if (S == 2) vstage<KW, DW, 2>(p, g, cur);
+                } else {
+                    if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
+                    if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
+                    if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+                }
             }
             if (wv == P - 1) {
                 const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
@@ -1557,6 +1628,19 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     }
 }
 
+// Vertical-first band kernel (4 words per lane): k = 8, 12 or 16 in one wave.
+template <bool C>
+static hipError_t launch_band_vf(int k, dim3 grid, const BitsArgs &a, hipStream_t s)
+{
+    switch (k) {
+    case 8: hipLaunchKernelGGL((band_step_kernel<8, 4, C, true>), grid, dim3(256), 0, s, a); break;
+    case 12: hipLaunchKernelGGL((band_step_kernel<12, 4, C, true>), grid, dim3(256), 0, s, a); break;
+    case 16: hipLaunchKernelGGL((band_step_kernel<16, 4, C, true>), grid, dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int DW, bool C>
 static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s)
 {
@@ -1594,6 +1678,18 @@ static hipError_t launch_band_split(bool contig, const BitsArgs &a, hipStream_t 
     return hipGetLastError();
 }
 
+// Vertical-first split pipeline: k = KW * P (VF stages hold 2 VGPRs per word and stage).
+template <int KW, int P>
+static hipError_t launch_band_pipe_vf(bool contig, const BitsArgs &a, hipStream_t s)
+{
+    const dim3 grid(a.ngroups, (int)((a.rows + a.strip - 1) / a.strip));
+    if (contig)
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), grid, dim3(64 * P), 0, s, a);
+    else
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), grid, dim3(64 * P), 0, s, a);
+    return hipGetLastError();
+}
+
 // Split-pipeline band step (k = 4 * waves per workgroup, 4 words per lane): 0 = off.
 int golk_band_split_enabled()
 {
@@ -1609,6 +1705,22 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
                           uint64_t *slots, hipStream_t s)
 {
     if (rows <= 0) return hipSuccess;
+    static const int vf = [] {  // vertical-first one-wave kernel for 4 words per lane
+        const char *e = getenv("GOL_BAND_VF");
+        return e ? atoi(e) : GOL_BAND_VF_DEFAULT;
+    }();
+    if (vf && dw == 4 && (k == 8 || k == 12 || k == 16)) {
+        BitsArgs a;
+        a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
+        a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
+        const int U = band_useful_words(k, 4);
+        a.ngroups = (int)((Wd + U - 1) / U);
+        a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
+        a.slots = slots;
+        const dim3 grid((a.ngroups + 3) / 4, (int)((rows + a.strip - 1) / a.strip));
+        const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
+        return contig ? launch_band_vf<true>(k, grid, a, s) : launch_band_vf<false>(k, grid, a, s);
+    }
     if (dw == 4 && (k == 12 || (golk_band_split_enabled() && (k == 8 || k == 16)))) {
         BitsArgs a;
         a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
@@ -1621,6 +1733,7 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
         a.slots = slots;
         const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
         if (k == 8) return launch_band_split<GOL_SPLIT_KW == 4 ? 4 : 2, GOL_SPLIT_KW == 4 ? 2 : 4>(contig, a, s);
+        if (k == 12 && GOL_PIPE_VF_DEFAULT) return launch_band_pipe_vf<12 / GOL_PIPE_VF_P, GOL_PIPE_VF_P>(contig, a, s);
         if (k == 12) return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s);
         return launch_band_split<4, 4>(contig, a, s);
     }

@@ -54,5 +54,7 @@ tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 t = json.load(open(tp)) if os.path.exists(tp) else {}
 if "hbm_bytes_per_launch" in out[main]:
     t[key] = {"kernel": main, "bytes_per_launch": out[main]["hbm_bytes_per_launch"], "profile": f"profiles/{tag}"}
+    if "valu_issue_frac" in out[main]:
+        t[key]["valu_issue_frac"] = round(out[main]["valu_issue_frac"], 4)
     json.dump(t, open(tp, "w"), indent=1)
 print(json.dumps(out[main], indent=1))
