@@ -432,3 +432,26 @@ def test_byte_board_k_turn_kernel(golhip, k):
     if ref is None:
         ref = O.run(board, turns)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("env", [{"GOL_BAND_VF": "1"}, {"GOL_SPLIT_SYNC": "0"}, {"GOL_BAND_SPLIT": "1"}])
+def test_alternative_band_kernels(golhip, env):
+    """The selectable alternatives of the band step (vertical-first one-wave kernel, barrier-
+    synchronised split pipeline, split pipeline at k = 8) against the bit oracle.  The switches
+    are read once per process, so each runs in a child process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import golhip\n"
+        "from oracle import oracle as O\n"
+        "for k in (8, 12):\n"
+        "    with golhip.Engine(140, 3072, device=0, turns_per_launch=k, layout='band') as e:\n"
+        "        e.load_random(31 + k)\n"
+        "        e.step(29)\n"
+        "        assert e.hash() == O.hash_words(O.bits_run(O.random_words(31 + k, 0, 140, 48), 29)), k\n"
+        "print('ok')\n" % (root, os.path.join(root, "gol-distributed-final_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
