@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--workload", default="weak", choices=["weak", "bit64k", "byte16k"])
     ap.add_argument("--k", type=int, default=0,
                     help="turns per launch (temporal blocking); 0 = library default for bit boards "
-                         "(12 band / 8 standard), 16 for byte16k")
+                         "(12 band / 8 standard), 32 for byte16k")
     ap.add_argument("--cpl", type=int, default=0, help="cells per lane (32/64/128; 0 = library default)")
     ap.add_argument("--strip", type=int, default=0, help="rows per wave strip (0 = auto)")
     ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"],
@@ -225,7 +225,7 @@ def run_bytes(args, rank, world):
     b = torch.empty_like(a)
     del bits
     stream = torch.cuda.current_stream().cuda_stream
-    k = max(kk for kk in (16, 8, 4, 2, 1) if kk <= args.k)
+    k = max(kk for kk in (32, 16, 8, 4, 2, 1) if kk <= args.k)
     pairs = []
     cur = [a, b]
 
@@ -272,7 +272,7 @@ def run_bytes(args, rank, world):
 def main():
     args = parse()
     if args.k <= 0 and args.workload == "byte16k":
-        args.k = 16  # bit boards: 0 = library default (12 on the band layout, 8 on the standard one)
+        args.k = 32  # pipelined byte kernel, 8 waves x 4 turns; bit boards: 0 = library default (12 on the band layout, 8 on the standard one)
     rank, world, local = setup(args)
     if args.workload == "byte16k":
         value, dt, cfg, roof, dtype = run_bytes(args, rank, world)

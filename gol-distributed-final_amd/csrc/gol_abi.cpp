@@ -657,7 +657,7 @@ extern "C" int gol_dev_bytes_step_k(const uint8_t *top, const uint8_t *mid, cons
                                     int32_t strip_rows, uint64_t *count_slots, void *stream)
 {
     if (!top || !mid || !bot || !dst || R <= 0 || W <= 0 || W % 32 || stride < W || stride % 16 || row0 < 0 ||
-        rows < 0 || row0 + rows > R || !(k == 1 || k == 2 || k == 4 || k == 8 || k == 16) || k > R ||
+        rows < 0 || row0 + rows > R || !(k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) || k > R ||
         (((uintptr_t)mid | (uintptr_t)top | (uintptr_t)bot | (uintptr_t)dst) & 15))
         return gol_set_error(GOL_EINVAL, "bad bytes_step_k arguments (R=%lld W=%lld stride=%lld k=%d)",
                              (long long)R, (long long)W, (long long)stride, k);

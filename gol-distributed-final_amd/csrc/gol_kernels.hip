@@ -980,10 +980,12 @@ band_pipe_kernel(BitsArgs a)
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[DW];
             {
-                v4u32 v = nextv;
+                // wait on the issued register itself (a copy taken before the wait would read
+                // the VGPR while the ds_read is in flight); row S+1 is read while row S computes
                 PT_BEGIN();
-                if (!(GOL_PIPE_ABL & 2)) lds_wait(v);  // block b row S is in VGPRs; row S+1 is read while row S computes
+                if (!(GOL_PIPE_ABL & 2)) lds_wait(nextv);
                 PT_END(pt_lds);
+                const v4u32 v = nextv;
                 if (S < 2) nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, S + 1));
                 cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
             }
@@ -1238,6 +1240,157 @@ __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
         }
     }
     if (a.slots) slot_add(a.slots, alive);
+}
+
+// Byte board, split pipeline: K = KW * P turns per launch, P waves per workgroup on one
+// column group of 62 words (32 cells per lane, standard bit layout in registers, shifted
+// frame), KW stages per wave, 3-row blocks handed on through LDS rings (256 B per row) with
+// the flag protocol of band_pipe_kernel.  Wave 0 loads and packs the bytes, wave P-1
+// realigns, unpacks and stores them.  One 32-cell word per lane covers K <= 32 columns of
+// halo, so K = 32 costs no more lanes than K = 16, and the 16384^2 board gets P waves per
+// column group instead of one (the one-wave kernel runs at ~1 wave per SIMD there).
+// Rows S = 0, 1, 2 of one ring slot (ROW = 64 uint32 apart), read and waited for together.
+__device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
+{
+    asm volatile(
+        "ds_read_b32 %0, %3\n\t"
+        "ds_read_b32 %1, %3 offset:256\n\t"
+        "ds_read_b32 %2, %3 offset:512\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
+        : "v"(p)
+        : "memory");
+}
+
+template <int KW, int P>
+__global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
+{
+    constexpr int K = KW * P;
+    static_assert(K <= 32, "one 32-cell halo word per side");
+    constexpr int NS = GOL_PIPE_SLOTS;
+    constexpr int ROW = 64;  // uint32 per LDS row
+    __shared__ uint32_t ring[P - 1][NS][3][ROW];
+    __shared__ int ready[P], consumed[P];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = blockIdx.x;
+    const int64_t col_raw = (int64_t)group * 62 + (lane - 1);
+    const int64_t col = ((col_raw % a.Wd) + a.Wd) % a.Wd;
+    const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
+    const int R = (int)a.R;
+    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
+    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
+    const int first_in = s0 - K, last_in = s1 + K - 1;
+    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
+    const int pitch = (int)a.pitch;
+    const char *mid_b = reinterpret_cast<const char *>(a.mid);
+    const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch;
+    const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch;
+    const uint32_t lane_off = (uint32_t)(col * 32);
+    char *dst_b = reinterpret_cast<char *>(a.dst);
+    const uint32_t row_bytes = (uint32_t)a.Wd * 32u;
+    const uint32_t st_off = writer ? lane_off : 0x80000000u;
+    const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
+
+    auto load = [&](int y, Raw32 &r) {  // wave 0
+        y = y > last_in ? last_in : y;
+        const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
+        const uint4 *q = reinterpret_cast<const uint4 *>(mid_b + (d + (int64_t)y * pitch) + lane_off);
+        r.lo = q[0];
+        r.hi = q[1];
+    };
+    auto store = [&](char *row, uint32_t nbytes, const uint32_t w) {  // wave P-1
+        uint4 lo, hi;
+        unpack32(w, lo, hi);
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, (int)nbytes, 0x00020000);
+        typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{lo.x, lo.y, lo.z, lo.w}, r, st_off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, hi.z, hi.w}, r, st_off + 16u, 0, 0);
+    };
+
+    if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
+    __syncthreads();
+    lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
+    lds_u32 *const ready_l = (lds_u32 *)&ready[0];
+    lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
+    auto slot_row = [&](int e, int b, int S) {  // ring e (input of wave e), e >= 1
+        return ring_l + (((e - 1) * NS + b % NS) * 3 + S) * ROW + lane;
+    };
+
+    typedef PipeSel<KW, 1, 1> PS;
+    typename PS::type p;
+    PS::init(p);
+    // wave 0: raw bytes of the current and the next block in registers (8 VGPRs per row)
+    Raw32 buf[2][3];
+    if (wv == 0) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) load(first_in + s, buf[0][s]);
+    }
+    uint32_t alive = 0;
+    bool ok = true;
+    int seen_ready = 0, seen_free = 0;
+    const uint32_t nrows = (uint32_t)(s1 - s0);
+    char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch;
+    auto block = [&](int b, auto par) {
+        constexpr int PAR = decltype(par)::value;  // wave 0's buffer of block b
+        if (wv == 0) {
+#pragma unroll
+            for (int s = 0; s < 3; ++s) load(first_in + 3 * (b + 1) + s, buf[1 - PAR][s]);  // clamped past the end
+        } else if (seen_ready < b + 1) {
+            seen_ready = spin_until_ge(ready_l + wv, b + 1);
+            ok = seen_ready >= 0;
+            if (!ok) return;
+        }
+        // the block's three rows, read and waited for in one asm statement: a split issue /
+        // wait lets the compiler copy the destination VGPR while the read is in flight (it did
+        // here; tools/check_lds_wait.py scans the assembly for that)
+        uint32_t rows3[3] = {0, 0, 0};
+        if (wv != 0) {
+            lds_rd32x3(slot_row(wv, b, 0), rows3);
+            if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
+        }
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+            uint32_t cur[1];
+            if (wv == 0) cur[0] = pack32(buf[PAR][S].lo, buf[PAR][S].hi);
+            else cur[0] = rows3[S];
+#pragma unroll
+            for (int g = 0; g < KW; ++g) {
+                if (S == 0) PS::template stage<0>(p, g, cur);
+                if (S == 1) PS::template stage<1>(p, g, cur);
+                if (S == 2) PS::template stage<2>(p, g, cur);
+            }
+            if (wv == P - 1) {
+                const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
+                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
+                // takes its shift mod 32)
+                const uint32_t nx = from_upper_lane(cur[0]);
+                const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, cur[0], K % 32) : nx;
+                store(srow, row_ok ? row_bytes : 0u, o);
+                srow += pitch;
+                if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
+            } else {
+                if (S == 0 && seen_free < b + 1 - NS) {
+                    seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    ok = seen_free >= 0;
+                    if (!ok) return;
+                }
+                lds_wr32(slot_row(wv + 1, b, S), (int)cur[0]);
+            }
+        }
+        if (wv < P - 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
+        }
+    };
+    int b = 0;
+    for (; b + 1 < nblk && ok; b += 2) {
+        block(b, std::integral_constant<int, 0>());
+        if (ok) block(b + 1, std::integral_constant<int, 1>());
+    }
+    if (b < nblk && ok) block(b, std::integral_constant<int, 0>());
+    if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
 
 // ------------------------------------------------------------------ byte-board step (exact semantics)
@@ -1632,10 +1785,16 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
 template <bool C>
 static hipError_t launch_band_vf(int k, dim3 grid, const BitsArgs &a, hipStream_t s)
 {
+    // GOL_BAND_LDS_PAD (bytes of unused dynamic LDS per workgroup) caps the workgroups per
+    // CU: an occupancy experiment knob (measurement only)
+    static const size_t pad = [] {
+        const char *e = getenv("GOL_BAND_LDS_PAD");
+        return e ? (size_t)atol(e) : (size_t)0;
+    }();
     switch (k) {
-    case 8: hipLaunchKernelGGL((band_step_kernel<8, 4, C, true>), grid, dim3(256), 0, s, a); break;
-    case 12: hipLaunchKernelGGL((band_step_kernel<12, 4, C, true>), grid, dim3(256), 0, s, a); break;
-    case 16: hipLaunchKernelGGL((band_step_kernel<16, 4, C, true>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((band_step_kernel<8, 4, C, true>), grid, dim3(256), pad, s, a); break;
+    case 12: hipLaunchKernelGGL((band_step_kernel<12, 4, C, true>), grid, dim3(256), pad, s, a); break;
+    case 16: hipLaunchKernelGGL((band_step_kernel<16, 4, C, true>), grid, dim3(256), pad, s, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1804,6 +1963,18 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
     if (rows <= 0) return hipSuccess;
     const int nstrips = (int)((rows + a.strip - 1) / a.strip);
     dim3 grid((a.ngroups + 3) / 4, nstrips);
+    static const int bpipe = [] {  // 1: k = 16 on the 4-wave byte pipeline too
+        const char *e = getenv("GOL_BYTES_PIPE16");
+        return e ? atoi(e) : 0;
+    }();
+    if (k == 32 || (k == 16 && bpipe)) {
+        // one workgroup of k/4 waves per (column group, strip); strips >= 8k rows
+        if (strip <= 0) a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
+        const dim3 g2(a.ngroups, (int)((rows + a.strip - 1) / a.strip));
+        if (k == 32) hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), g2, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((bytes_pipe_kernel<4, 4>), g2, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     switch (k) {
     case 1: hipLaunchKernelGGL(bytes_blocked_kernel<1>, grid, dim3(256), 0, s, a); break;
     case 2: hipLaunchKernelGGL(bytes_blocked_kernel<2>, grid, dim3(256), 0, s, a); break;

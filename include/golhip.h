@@ -169,7 +169,8 @@ int gol_dev_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch,
 int gol_dev_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t stride, int64_t y0,
                        int64_t y1, uint8_t *out, int64_t out_stride, void *stream);
 
-/* k turns (1, 2, 4, 8 or 16) of a byte board whose bytes are all 0 or 255 (every
+/* k turns (1, 2, 4, 8, 16 or 32; 32 runs as 8 waves x 4 turns of one workgroup, the
+ * byte pipeline) of a byte board whose bytes are all 0 or 255 (every
  * board after its first turn), W % 32 == 0, stride % 16 == 0, 16-byte aligned
  * rows; row addressing as gol_dev_bits_step (top/mid/bot are byte rows, pitch
  * `stride`).  Same results as k exact turns on such boards; 2 bytes of HBM

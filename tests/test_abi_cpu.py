@@ -117,3 +117,16 @@ def test_stub_names_match_reference(G):
     res = s.Response()
     for f in ["Alive", "AliveCount", "TurnsCompleted", "World", "WorkSlice", "Worker"]:
         assert hasattr(res, f)
+
+
+def test_pipe_kernels_wait_before_reading_lds(tmp_path):
+    """The pipe kernels' inline-asm LDS reads: no instruction may read a destination
+    VGPR before its s_waitcnt (a compiler copy there read stale rows once:
+    tools/check_lds_wait.py).  Compiles gol_kernels.hip to gfx950 assembly (~20 s)."""
+    import shutil
+    if shutil.which("/opt/rocm/bin/hipcc") is None:
+        pytest.skip("hipcc not present")
+    r = subprocess.run(["python", os.path.join(ROOT, "tools", "check_lds_wait.py")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "0 hazards" in r.stdout

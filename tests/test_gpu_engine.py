@@ -408,7 +408,7 @@ def test_alive_events_during_run_pause_quit(golhip, golden_dir):
         ops.Run(golhip.Request(World=board, Turns=1, ImageHeight=512, ImageWidth=512, Threads=1))
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32])
 def test_byte_board_k_turn_kernel(golhip, k):
     """gol_dev_bytes_step_k (0/255 byte board, k turns per launch) against the oracle, with the
     torus wrap through top/bot and a split into two launches (row ranges)."""
@@ -454,4 +454,31 @@ def test_alternative_band_kernels(golhip, env):
         "print('ok')\n" % (root, os.path.join(root, "gol-distributed-final_amd")))
     r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
                        timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_byte_pipe_k16_switch(golhip):
+    """GOL_BYTES_PIPE16=1 runs k = 16 on the 4-wave byte pipeline (child process: the switch is
+    read once per process); exact against the oracle with a two-launch row split."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import numpy as np, torch\n"
+        "from golhip._lib import check, lib\n"
+        "from oracle import oracle as O\n"
+        "H, W, k = 150, 32 * 40, 16\n"
+        "board = (np.random.default_rng(3).random((H, W)) < 0.4).astype(np.uint8) * 255\n"
+        "a = torch.from_numpy(board).cuda(); b = torch.empty_like(a)\n"
+        "st = torch.cuda.current_stream().cuda_stream\n"
+        "for _ in range(2):\n"
+        "    top = a[H - k:]\n"
+        "    check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W, 0, 70, k, 0, None, st))\n"
+        "    check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W, 70, H - 70, k, 0, None, st))\n"
+        "    a, b = b, a\n"
+        "assert np.array_equal(a.cpu().numpy(), O.run(board, 2 * k))\n"
+        "print('ok')\n" % (root, os.path.join(root, "gol-distributed-final_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "GOL_BYTES_PIPE16": "1"},
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

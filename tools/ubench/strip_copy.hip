@@ -7,7 +7,9 @@
 #include <stdint.h>
 #include <stdio.h>
 
-template <int WPB>
+// TILED: the board stored chunk-major (all rows of a 1 KiB column chunk contiguous), so a
+// wave's strip is one sequential stream.
+template <int WPB, bool TILED>
 __global__ void __launch_bounds__(64 * WPB) copy_kernel(const uint4 *src, uint4 *dst, int rows, int strip,
                                                          int chunks_per_row)
 {
@@ -16,8 +18,8 @@ __global__ void __launch_bounds__(64 * WPB) copy_kernel(const uint4 *src, uint4 
     if (chunk >= chunks_per_row) return;
     const int r0 = blockIdx.y * strip;
     const int r1 = min(r0 + strip, rows);
-    const int64_t pitch = (int64_t)chunks_per_row * 64;  // uint4 per row
-    const int64_t col = (int64_t)chunk * 64 + lane;
+    const int64_t pitch = TILED ? 64 : (int64_t)chunks_per_row * 64;  // uint4 per row
+    const int64_t col = TILED ? (int64_t)chunk * rows * 64 + lane : (int64_t)chunk * 64 + lane;
     uint4 b0 = src[(int64_t)r0 * pitch + col];
     uint4 b1 = r0 + 1 < r1 ? src[(int64_t)(r0 + 1) * pitch + col] : b0;
     uint4 b2 = r0 + 2 < r1 ? src[(int64_t)(r0 + 2) * pitch + col] : b0;
@@ -31,11 +33,11 @@ __global__ void __launch_bounds__(64 * WPB) copy_kernel(const uint4 *src, uint4 
     }
 }
 
-template <int WPB>
+template <int WPB, bool TILED = false>
 void run(const uint4 *src, uint4 *dst, int rows, int cpr, int strip)
 {
     const dim3 grid((cpr + WPB - 1) / WPB, (rows + strip - 1) / strip);
-    hipLaunchKernelGGL((copy_kernel<WPB>), grid, dim3(64 * WPB), 0, 0, src, dst, rows, strip, cpr);
+    hipLaunchKernelGGL((copy_kernel<WPB, TILED>), grid, dim3(64 * WPB), 0, 0, src, dst, rows, strip, cpr);
     (void)hipDeviceSynchronize();
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
@@ -43,13 +45,14 @@ void run(const uint4 *src, uint4 *dst, int rows, int cpr, int strip)
     (void)hipEventRecord(e0);
     const int reps = 5;
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((copy_kernel<WPB>), grid, dim3(64 * WPB), 0, 0, src, dst, rows, strip, cpr);
+        hipLaunchKernelGGL((copy_kernel<WPB, TILED>), grid, dim3(64 * WPB), 0, 0, src, dst, rows, strip, cpr);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
     const double bytes = 2.0 * rows * (double)cpr * 1024 * reps;
-    printf("waves/WG %2d strip %5d: %.0f GB/s (read + write)\n", WPB, strip, bytes / (ms * 1e-3) / 1e9);
+    printf("%s waves/WG %2d strip %5d: %.0f GB/s (read + write)\n", TILED ? "tiled  " : "rowmajor", WPB, strip,
+           bytes / (ms * 1e-3) / 1e9);
 }
 
 int main()
@@ -63,8 +66,9 @@ int main()
     (void)hipMemset(src, 0x5a, (size_t)rows * cpr * 1024);
     for (int strip : {512, 1024}) {
         run<4>(src, dst, rows, cpr, strip);
-        run<8>(src, dst, rows, cpr, strip);
         run<16>(src, dst, rows, cpr, strip);
+        run<1, true>(src, dst, rows, cpr, strip);
+        run<4, true>(src, dst, rows, cpr, strip);
     }
     return 0;
 }
