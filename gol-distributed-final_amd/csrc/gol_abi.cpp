@@ -590,7 +590,7 @@ extern "C" int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const
     const int dw = cells_per_lane == 64 ? 2 : (cells_per_lane == 128 ? 4 : (cells_per_lane <= 0 ? GOL_BAND_DEFAULT_DW : 0));
     if (!top || !mid || !bot || !dst || R <= 0 || Wd <= 0 || !dw || Wd % dw || pitch < Wd || pitch % dw ||
         row0 < 0 || rows < 0 || row0 + rows > R ||
-        !(k == 1 || k == 2 || k == 4 || k == 8 || (k == 16 && dw == 2) || (k == 12 && dw == 4)) ||
+        !(k == 1 || k == 2 || k == 4 || k == 8 || (k == 16 && dw == 2) || ((k == 12 || k == 24) && dw == 4)) ||
         k > R || (((uintptr_t)mid | (uintptr_t)top | (uintptr_t)bot | (uintptr_t)dst) & (4 * dw - 1)))
         return gol_set_error(GOL_EINVAL, "bad band_step arguments (R=%lld Wd=%lld pitch=%lld k=%d cells_per_lane=%d)",
                              (long long)R, (long long)Wd, (long long)pitch, k, cells_per_lane);

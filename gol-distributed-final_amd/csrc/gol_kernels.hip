@@ -371,12 +371,21 @@ bits_step_kernel(BitsArgs a)
 // Store DW words at byte offset voff of a buffer [row, row + nbytes): out-of-range
 // offsets (and nbytes = 0) are dropped by the hardware range check.
 template <int DW>
+#ifndef GOL_ST_AUX
+#define GOL_ST_AUX 2  // nt (streaming) stores: +1 % measured; cache-policy bits of the band kernels' row stores (measurement knob)
+#endif
+#ifndef GOL_XCD_REMAP
+#define GOL_XCD_REMAP 1  // pipe kernel: contiguous runs of column groups per XCD
+#endif
+#ifndef GOL_LD_AUX
+#define GOL_LD_AUX 0  // cache-policy bits of the pipe kernel's global_load_lds (measurement knob)
+#endif
 __device__ __forceinline__ void store_row_masked(char *row, uint32_t nbytes, uint32_t voff, const uint32_t (&w)[DW])
 {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, (int)nbytes, 0x00020000);
     if constexpr (DW == 4) {
         typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, r, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, r, voff, 0, GOL_ST_AUX);
     } else if constexpr (DW == 2) {
         typedef __attribute__((ext_vector_type(2))) uint32_t v2u;
         __builtin_amdgcn_raw_buffer_store_b64(v2u{w[0], w[1]}, r, voff, 0, 0);
@@ -812,6 +821,12 @@ band_split_kernel(BitsArgs a)
 #ifndef GOL_PIPE_SLOTS
 #define GOL_PIPE_SLOTS 3
 #endif
+#ifndef GOL_PIPE_PRIO
+#define GOL_PIPE_PRIO 0  // wave priority by role: 0 = equal, 1 = upstream first, 2 = downstream first
+#endif
+#ifndef GOL_PIPE_LGKM
+#define GOL_PIPE_LGKM 1  // per-role loops with partial LDS waits and row-0 prefetch (0 = previous loop)
+#endif
 // LDS accesses of the pipeline are inline asm: the compiler treats a global_load_lds in
 // flight as a pending LDS write and would put vmcnt(0) before every LDS access it can see
 // (which, on the storing wave, also waits for its HBM stores).  Each read waits for its own
@@ -833,6 +848,16 @@ __device__ __forceinline__ v4u32 lds_rd128_issue(const lds_u32 *p)
     return r;
 }
 __device__ __forceinline__ void lds_wait(v4u32 &r) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r)::"memory"); }
+// Wait for a read with N younger LDS operations allowed in flight (LDS operations of a wave
+// complete in order, and these kernels issue no scalar loads in the loop; the assembly check
+// tools/check_lds_wait.py confirms the latter).
+template <int N>
+__device__ __forceinline__ void lds_wait_n(v4u32 &r)
+{
+    if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r)::"memory");
+    else asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(r)::"memory");
+}
+__device__ __forceinline__ void lds_wait1() { asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory"); }
 __device__ __forceinline__ void lds_wr128(lds_u32 *p, v4u32 v)
 {
     asm volatile("ds_write_b128 %0, %1" ::"v"(p), "v"(v) : "memory");
@@ -857,7 +882,8 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 }
 
 template <int KW, int P, bool CONTIG, bool VF = false>
-__global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(GOL_SPLIT_MIN_WAVES, 8)))
+__global__ void __launch_bounds__(64 * P)
+__attribute__((amdgpu_waves_per_eu(KW >= 4 && !VF ? 3 : GOL_SPLIT_MIN_WAVES, 8)))  // 5 KW DW pipeline VGPRs
 band_pipe_kernel(BitsArgs a)
 {
     constexpr int DW = 4;
@@ -875,8 +901,21 @@ band_pipe_kernel(BitsArgs a)
     // Pipeline position of this wave.  Rotated by workgroup: the waves of a workgroup sit on
     // the CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put
     // its loader (global_load_lds) on one SIMD and its storer on another.
-    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + GOL_PIPE_ROTATE * (blockIdx.x + blockIdx.y)) % P);
-    const int group = blockIdx.x;
+    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (L2 per XCD), so
+    // consecutive ids are remapped to let each XCD walk its own contiguous run of column groups
+    // of a strip: the lateral halo columns two neighbouring groups both read then meet in one L2.
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (GOL_XCD_REMAP) {
+        const int n = gridDim.x * gridDim.y, l = blockIdx.x + blockIdx.y * gridDim.x;
+        const int per = n / 8;
+        if (l < per * 8) {
+            const int m = (l % 8) * per + l / 8;
+            bx = m % gridDim.x;
+            by = m / gridDim.x;
+        }
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + GOL_PIPE_ROTATE * (bx + by)) % P);
+    const int group = bx;
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
     const int64_t q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
@@ -886,7 +925,7 @@ band_pipe_kernel(BitsArgs a)
     const bool writer = lane >= HL && lane < 64 - HL && col_raw < a.Wd;
 
     const int R = (int)a.R;
-    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
+    const int s0 = (int)a.row0 + by * a.strip;
     const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
     const int first_in = s0 - K;
     const int last_in = s1 + K - 1;
@@ -910,7 +949,7 @@ band_pipe_kernel(BitsArgs a)
             y = y > last_in ? last_in : y;
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, GOL_LD_AUX);
         }
     };
 
@@ -959,6 +998,120 @@ band_pipe_kernel(BitsArgs a)
 #define PT_BEGIN()
 #define PT_END(acc)
 #endif
+#if GOL_PIPE_LGKM
+    // One loop per role (0 = loader, 1 = middle, 2 = storer), so every LDS wait has a count
+    // known at compile time.  Row S+1 is read while row S computes; a row wait lets the one
+    // younger LDS operation (the previous row's ds_write) stay in flight instead of draining
+    // it (lgkmcnt(1)); the middle and last waves read row 0 of the next block during row 2
+    // when its flag is already known to be set; "block b-1 ready" is published after row 0
+    // of block b, by when block b-1's writes have completed.
+    auto role_loop = [&](auto role_c) {
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool WRITES = ROLE != 2;  // writes the next wave's ring
+        if constexpr (GOL_PIPE_PRIO == 1) __builtin_amdgcn_s_setprio(ROLE == 0 ? 3 : (ROLE == 1 ? 2 : 0));
+        if constexpr (GOL_PIPE_PRIO == 2) __builtin_amdgcn_s_setprio(ROLE == 2 ? 3 : (ROLE == 1 ? 1 : 0));
+        v4u32 nextv = fake;
+        bool pre = false;  // row 0 of block b already issued into nextv
+        for (int b = 0; b < nblk; ++b) {
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+                uint32_t cur[DW];
+                v4u32 v;
+                if (S == 0) {
+                    PT_BEGIN();
+                    if (ROLE == 0) {
+                        // block b landed; blocks b+1 .. b+NSI-2 (if any) may stay in flight
+                        const int inflight = min(NSI - 2, nblk - 1 - b);
+                        if (inflight >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+                        else if (inflight == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                        else if (inflight == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    if (ROLE != 0 && pre) {
+                        lds_wait_n<1>(nextv);  // younger: the previous block's row 2 write / consumed flag
+                        v = nextv;
+                    } else {
+                        if (ROLE != 0 && seen_ready < b + 1) {
+                            seen_ready = spin_until_ge(ready_l + wv, b + 1);
+                            if (seen_ready < 0) { ok = false; return; }
+                        }
+                        v = lds_rd128(slot_row(wv, b, 0));
+                    }
+                    PT_END(pt_in);
+                } else {
+                    PT_BEGIN();
+                    lds_wait_n<WRITES ? 1 : 0>(nextv);  // younger: row S-1's write
+                    PT_END(pt_lds);
+                    v = nextv;
+                }
+                if (S < 2) {
+                    nextv = lds_rd128_issue(slot_row(wv, b, S + 1));
+                } else {
+                    pre = false;
+                    if (ROLE != 0 && b + 1 < nblk && seen_ready >= b + 2) {
+                        nextv = lds_rd128_issue(slot_row(wv, b + 1, 0));
+                        pre = true;
+                    }
+                    if (ROLE == 0) {
+                        if (b + NSI - 1 < nblk) stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);  // refills slot (b-1) % NSI
+                    } else if (lane == 0) {
+                        lds_wr32(consumed_l + wv, b + 1);
+                    }
+                }
+                cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
+                if (ROLE == 0 && wrap) {
+#pragma unroll
+                    for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
+                }
+#pragma unroll
+                for (int g = 0; g < KW; ++g) {
+                    if constexpr (VF) {
+                        if (S == 0) vstage<KW, DW, 0>(p, g, cur);
+                        if (S == 1) vstage<KW, DW, 1>(p, g, cur);
+                        if (S == 2) vstage<KW, DW, 2>(p, g, cur);
+                    } else {
+                        if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
+                        if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
+                        if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+                    }
+                }
+                if constexpr (!WRITES) {
+                    const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
+                    store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
+                    srow += pitch_b;
+                    if (a.slots) {
+                        uint32_t c = 0;
+#pragma unroll
+                        for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
+                        alive += bitop3<0x80>(c, st_mask, row_ok ? 0xFFFFFFFFu : 0u);  // c & writer & row_ok
+                    }
+                } else {
+                    if (S == 0) {
+                        if (b > 0) {
+                            lds_wait1();  // all but the row-1 read: block b-1's row writes are done
+                            if (lane == 0) lds_wr32(ready_l + wv + 1, b);
+                        }
+                        if (seen_free < b + 1 - NS) {  // slot b % NS of ring wv+1 free: block b-NS consumed
+                            PT_BEGIN();
+                            seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                            PT_END(pt_free);
+                            if (seen_free < 0) { ok = false; return; }
+                        }
+                    }
+                    lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
+                }
+            }
+        }
+        if (WRITES) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows written before the flag
+            if (lane == 0) lds_wr32(ready_l + wv + 1, nblk);
+        }
+    };
+    (void)ok;
+    if (wv == 0) role_loop(std::integral_constant<int, 0>());
+    else if (wv == P - 1) role_loop(std::integral_constant<int, 2>());
+    else role_loop(std::integral_constant<int, 1>());
+#else
     for (int b = 0; b < nblk && ok; ++b) {
         // input block b
         PT_BEGIN();
@@ -1040,6 +1193,7 @@ band_pipe_kernel(BitsArgs a)
             if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
         }
     }
+#endif
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if GOL_PIPE_PROFILE
     // diagnostic build only: per-role cycle sums in slots[role*64 + 8*i] (i: total, input wait,
@@ -1880,7 +2034,7 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
         const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
         return contig ? launch_band_vf<true>(k, grid, a, s) : launch_band_vf<false>(k, grid, a, s);
     }
-    if (dw == 4 && (k == 12 || (golk_band_split_enabled() && (k == 8 || k == 16)))) {
+    if (dw == 4 && (k == 12 || k == 24 || (golk_band_split_enabled() && (k == 8 || k == 16)))) {
         BitsArgs a;
         a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
         a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
@@ -1893,7 +2047,16 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
         const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
         if (k == 8) return launch_band_split<GOL_SPLIT_KW == 4 ? 4 : 2, GOL_SPLIT_KW == 4 ? 2 : 4>(contig, a, s);
         if (k == 12 && GOL_PIPE_VF_DEFAULT) return launch_band_pipe_vf<12 / GOL_PIPE_VF_P, GOL_PIPE_VF_P>(contig, a, s);
-        if (k == 12) return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s);
+        if (k == 12) {
+            static const int shape = [] {  // waves per workgroup for k = 12 (measurement knob)
+                const char *e = getenv("GOL_PIPE_WAVES");
+                return e ? atoi(e) : 12 / GOL_SPLIT_KW;
+            }();
+            if (shape == 3) return launch_band_split<4, 3>(contig, a, s);
+            if (shape == 2) return launch_band_split<6, 2>(contig, a, s);
+            return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s);
+        }
+        if (k == 24) return launch_band_split<3, 8>(contig, a, s);  // 8 waves x 3 stages
         return launch_band_split<4, 4>(contig, a, s);
     }
     BitsArgs a;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library builds on one GPU box: tools/ab.sh "<sweep variants>" libA.so libB.so ...
-# Runs tools/sweep.py for every library in turn, twice, so box-to-box clock differences
+# (build the libraries with tools/build_variant.sh.)  Runs tools/sweep.py for every library in turn, twice, so box-to-box clock differences
 # cancel out of the comparison.  Output: gpurun_out/ab.log
 set -o pipefail
 V=$1; shift

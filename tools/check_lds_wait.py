@@ -52,43 +52,53 @@ def kernels(asm, pattern):
 
 
 def check(body):
-    """Straight-line scan: after an asm ds_read, any use of its destination before an
-    lgkmcnt(0) wait is a hazard.  Branch targets reset the in-flight set only when a wait
-    is seen, so a hazard across a label is still reported (conservative)."""
+    """Straight-line scan of the LDS counter: outstanding LDS operations are kept in issue
+    order (they complete in order); `s_waitcnt lgkmcnt(N)` retires all but the youngest N.
+    A vector instruction that reads the destination of an outstanding ds_read is a hazard,
+    and so is a partial wait (N > 0) while a scalar load is outstanding (scalar loads share
+    the counter but complete out of order).  Labels do not reset the state, so the scan is
+    an approximation of the control flow: straight-line and fall-through paths are tracked,
+    code after an unconditional branch starts from an empty counter."""
     hazards = []
-    pending = {}  # vgpr -> line of the ds_read
-    in_asm = False
+    out = []  # (kind, regs) in issue order
     for i, line in enumerate(body.splitlines()):
         s = line.split(";")[0].strip()
-        if ";;#ASMSTART" in line:
-            in_asm = True
-            continue
-        if ";;#ASMEND" in line:
-            in_asm = False
-            continue
         if not s or s.endswith(":") or s.startswith("."):
             continue
         op, _, rest = s.partition(" ")
-        if op == "s_waitcnt" and "lgkmcnt(0)" in rest:
-            pending.clear()
+        if op == "s_waitcnt":
+            m = re.search(r"lgkmcnt\((\d+)\)", rest)
+            if m:
+                n = int(m.group(1))
+                if n < len(out):
+                    if n > 0 and any(k == "smem" for k, _ in out):
+                        hazards.append((i, s, ["partial lgkmcnt wait with a scalar load outstanding"]))
+                    out = out[len(out) - n:] if n else []
             continue
-        if op.startswith("ds_read") and in_asm:
-            dst, _, src = rest.partition(",")
-            for r in regs(dst):
-                pending[r] = i
+        if op.startswith(("s_load", "s_buffer_load")):
+            out.append(("smem", set()))
+            continue
+        if op in ("s_branch", "s_setpc_b64"):
+            out = []  # the next instruction is reached from elsewhere: state unknown, assume drained
             continue
         if op.startswith("s_"):
             continue
-        # sources: everything after the first operand for VALU / stores; all operands for
-        # stores and ds_write (they have no destination VGPR)
-        if op.startswith(("ds_write", "buffer_store", "global_store", "flat_store")):
+        pending = set().union(*(r for _, r in out)) if out else set()
+        if op.startswith("ds_read"):
+            dst, _, src = rest.partition(",")
+            used = regs(src)
+        elif op.startswith(("ds_write", "buffer_store", "global_store", "flat_store")):
             used = regs(rest)
         else:
             _, _, srcs = rest.partition(",")
             used = regs(srcs)
-        bad = used & pending.keys()
+        bad = used & pending
         if bad:
             hazards.append((i, s, sorted(bad)))
+        if op.startswith("ds_read"):
+            out.append(("ds", regs(dst)))
+        elif op.startswith("ds_"):
+            out.append(("ds", set()))
     return hazards
 
 

@@ -4,11 +4,21 @@
 //   hipcc --offload-arch=gfx950 -O3 -I../../include -I../../gol-distributed-final_amd/csrc pipe_compute.hip -o pipe_compute
 #include "gol_kernels.hip"
 
-template <int KW>
+// MODE 0: compute only.  MODE 1: + the pipe kernel's LDS hand-off per row (ds_write_b128 of
+// the row's result, ds_read_b128 of the next row issued one row ahead, waited with
+// lgkmcnt(1)), on the wave's own slot so there is no cross-wave waiting.  MODE 2: + one
+// 16-byte global store per row (a buffer store, like the last wave).  MODE 3: both.
+template <int KW, int MODE = 0>
 __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, int iters)
 {
     using namespace golk;
     constexpr int DW = 4;
+    __shared__ uint32_t ring[4][3][3][256];
+    lds_u32 *const slot = (lds_u32 *)&ring[threadIdx.x >> 6][0][0][0] + (threadIdx.x & 63) * 4;
+    v4u32 nextv = v4u32{threadIdx.x, 1u, 2u, 3u};
+    if (MODE & 1) lds_wr128(slot, nextv);
+    if (MODE & 1) nextv = lds_rd128_issue(slot);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);  // range 0: dropped
     Pipe<KW, DW> p;
     PipeSel<KW, DW, 0>::init(p);
     uint32_t seed = threadIdx.x * 2654435761u + blockIdx.x;
@@ -18,8 +28,16 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[DW];
+            if (MODE & 1) {
+                lds_wait_n<1>(nextv);
+                const v4u32 v = nextv;
+                nextv = lds_rd128_issue(slot + ((S + 1) % 3) * 256);
 #pragma unroll
-            for (int j = 0; j < DW; ++j) cur[j] = seed ^ (it * 3 + S + j);
+                for (int j = 0; j < DW; ++j) cur[j] = v[j] ^ (it * 3 + S + j);
+            } else {
+#pragma unroll
+                for (int j = 0; j < DW; ++j) cur[j] = seed ^ (it * 3 + S + j);
+            }
 #pragma unroll
             for (int g = 0; g < KW; ++g) {
                 if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
@@ -28,14 +46,23 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
             }
 #pragma unroll
             for (int j = 0; j < DW; ++j) acc ^= cur[j];
+            if (MODE & 1) lds_wr128(slot + S * 256, v4u32{cur[0], cur[1], cur[2], cur[3]});
+            if (MODE & 2) {
+                typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{cur[0], cur[1], cur[2], cur[3]}, rs, (threadIdx.x & 63) * 16, 0, 0);
+            }
         }
+    }
+    if (MODE & 1) {
+        lds_wait(nextv);
+        acc ^= nextv.x;
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
     if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
 }
 
-template <int KW>
+template <int KW, int MODE = 0>
 void run(int wps)
 {
     const int blocks = 256 * wps, iters = 2000;
@@ -43,8 +70,8 @@ void run(int wps)
     uint64_t *cyc;
     (void)hipMalloc(&out, (size_t)blocks * 256 * 4);
     (void)hipMalloc(&cyc, (size_t)blocks * 4 * 8);
-    hipLaunchKernelGGL((pc_kernel<KW>), dim3(blocks), dim3(256), 0, 0, out, cyc, 10);
-    hipLaunchKernelGGL((pc_kernel<KW>), dim3(blocks), dim3(256), 0, 0, out, cyc, iters);
+    hipLaunchKernelGGL((pc_kernel<KW, MODE>), dim3(blocks), dim3(256), 0, 0, out, cyc, 10);
+    hipLaunchKernelGGL((pc_kernel<KW, MODE>), dim3(blocks), dim3(256), 0, 0, out, cyc, iters);
     (void)hipDeviceSynchronize();
     uint64_t *h = (uint64_t *)malloc((size_t)blocks * 4 * 8);
     (void)hipMemcpy(h, cyc, (size_t)blocks * 4 * 8, hipMemcpyDeviceToHost);
@@ -53,7 +80,7 @@ void run(int wps)
     mean /= blocks * 4;
     // VALU per row and stage: 10 logic + 2/4 DPP (approx); report cycles per word-generation
     const double wordgens = (double)iters * 3 * KW * 4;
-    printf("KW=%d waves/SIMD=%d  SIMD cycles per word-generation=%.2f\n", KW, wps, mean / wordgens / wps);
+    printf("KW=%d mode=%d waves/SIMD=%d  SIMD cycles per word-generation=%.2f\n", KW, MODE, wps, mean / wordgens / wps);
     free(h);
     (void)hipFree(out);
     (void)hipFree(cyc);
@@ -61,9 +88,12 @@ void run(int wps)
 
 int main()
 {
-    for (int w : {2, 4}) {
-        run<3>(w);
-        run<8>(w);
-    }
+    for (int rep = 0; rep < 2; ++rep)
+        for (int w : {2, 4}) {
+            run<3, 0>(w);
+            run<3, 1>(w);
+            run<3, 2>(w);
+            run<3, 3>(w);
+        }
     return 0;
 }
