@@ -15,6 +15,8 @@
 // wave_shr:1 / wave_shl:1; lanes 0 and 63 of every wave are halo lanes whose
 // results are discarded (the halo is one word = 32 cells >= K).
 #include <hip/hip_runtime.h>
+#include <map>
+#include <mutex>
 #include <stdint.h>
 
 #include <stdlib.h>
@@ -825,7 +827,7 @@ band_split_kernel(BitsArgs a)
 #define GOL_PIPE_PRIO 0  // wave priority by role: 0 = equal, 1 = upstream first, 2 = downstream first
 #endif
 #ifndef GOL_PIPE_LGKM
-#define GOL_PIPE_LGKM 1  // per-role loops with partial LDS waits and row-0 prefetch (0 = previous loop)
+#define GOL_PIPE_LGKM 2  // 2: per-role loops unrolled over the ring slots; 1: per-role loops; 0: first loop
 #endif
 // LDS accesses of the pipeline are inline asm: the compiler treats a global_load_lds in
 // flight as a pending LDS write and would put vmcnt(0) before every LDS access it can see
@@ -858,6 +860,23 @@ __device__ __forceinline__ void lds_wait_n(v4u32 &r)
     else asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(r)::"memory");
 }
 __device__ __forceinline__ void lds_wait1() { asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory"); }
+// Immediate-offset forms (byte offsets < 64 KiB): ring slots and rows at compile-time offsets
+// from one per-lane address register.
+template <int OFF>
+__device__ __forceinline__ v4u32 lds_rd128_issue_o(const lds_u32 *p)
+{
+    v4u32 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(p), "i"(OFF) : "memory");
+    return r;
+}
+template <int OFF>
+__device__ __forceinline__ void lds_wr128_o(lds_u32 *p, v4u32 v)
+{
+    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(p), "v"(v), "i"(OFF) : "memory");
+}
+// Flag write without an exec mask: lane 0's address is the flag, the other lanes write their
+// own scratch word (one ds_write, no saveexec / branch around it).
+__device__ __forceinline__ void lds_flag_wr(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
 __device__ __forceinline__ void lds_wr128(lds_u32 *p, v4u32 v)
 {
     asm volatile("ds_write_b128 %0, %1" ::"v"(p), "v"(v) : "memory");
@@ -873,6 +892,7 @@ __device__ __forceinline__ void lds_wr32(lds_u32 *p, int v) { asm volatile("ds_w
 // several blocks ahead, so most blocks need no flag read), or -1 after the spin bound.
 __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 {
+#pragma clang loop unroll(disable)
     for (int n = 0; n < (1 << 22); ++n) {
         const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
         if (x >= v) return x;
@@ -896,6 +916,8 @@ band_pipe_kernel(BitsArgs a)
     __shared__ uint32_t in_ring[NSI][3][ROW];
     __shared__ uint32_t ring[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
     __shared__ int ready[P], consumed[P];
+    __shared__ int flag_scratch[GOL_PIPE_LGKM == 2 ? P : 1][64];
+    (void)flag_scratch;
 
     const int lane = threadIdx.x & 63;
     // Pipeline position of this wave.  Rotated by workgroup: the waves of a workgroup sit on
@@ -939,6 +961,7 @@ band_pipe_kernel(BitsArgs a)
     char *dst_b = reinterpret_cast<char *>(a.dst);
     const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
+    (void)row_bytes;
 
     // wave 0: block b -> in_ring[b % NSI] (global_load_lds).  The slot is an argument: a lambda
     // that captures a __shared__ array silently loses the kernel's host-side stub.
@@ -998,7 +1021,154 @@ band_pipe_kernel(BitsArgs a)
 #define PT_BEGIN()
 #define PT_END(acc)
 #endif
-#if GOL_PIPE_LGKM
+#if GOL_PIPE_LGKM == 2
+    // One loop per role (0 = loader, 1 = middle, 2 = last), unrolled over the 3 ring slots so
+    // every LDS address is a per-lane register plus an immediate offset and every wait count is
+    // a constant.  The loop carries no other per-block arithmetic than the flag values:
+    // the per-block instruction count is what bounds this kernel (all waves issue through the
+    // same per-SIMD slots, so scalar and branch instructions cost about as much as VALU ones).
+    //  * row S+1 is read while row S computes; a row wait leaves the youngest LDS operation
+    //    (this wave's previous ds_write or flag write) in flight: lgkmcnt(1);
+    //  * the reading waves issue row 0 of block b+1 at row 2 of block b (spinning there if its
+    //    flag is not yet seen), then write "block b consumed";
+    //  * a writing wave publishes "blocks < b ready" after computing row 0 of block b, when its
+    //    writes of block b-1 are done (lgkmcnt(1) leaves only the row-1 read in flight);
+    //  * the block count is padded to a multiple of 3: padding blocks read clamped rows and
+    //    their stores fall outside the strip's buffer range.
+    static_assert(NS == 3 && NSI == 3, "the unrolled loop assumes 3-slot rings");
+    (void)ok; (void)fake; (void)slot_row; (void)srow; (void)st_mask;
+    const int nblk3 = (nblk + 2) / 3 * 3;
+    constexpr int SB = SLOT * 4, RB = ROW * 4;  // slot and row strides in bytes
+    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0][0] + (GOL_PIPE_LGKM == 2 ? wv : 0) * 64 + lane;
+    lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;      // writer: ring wv+1 ready
+    lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;       // reader: ring wv consumed
+    lds_u32 *const in_base = in_l + lane * 4;
+    lds_u32 *const rd_base = ring_l + (wv - 1) * NS * SLOT + lane * 4;  // ring wv (wv >= 1)
+    lds_u32 *const wr_base = ring_l + wv * NS * SLOT + lane * 4;        // ring wv+1 (wv < P-1)
+    auto compute = [&](auto s_c, uint32_t (&cur)[DW]) {
+        constexpr int S = decltype(s_c)::value;
+#pragma unroll
+        for (int g = 0; g < KW; ++g) {
+            if constexpr (VF) vstage<KW, DW, S>(p, g, cur);
+            else bstage_seq<KW, DW, S>(p, g, cur);
+        }
+    };
+    auto unpack = [&](const v4u32 v, uint32_t (&cur)[DW]) { cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w; };
+    auto pack = [&](const uint32_t (&cur)[DW]) { return v4u32{cur[0], cur[1], cur[2], cur[3]}; };
+    // writer, after row 0 of block b: publish blocks < b, then make sure slot b % 3 is free
+    auto publish_and_reserve = [&](int b) -> bool {
+        lds_wait1();
+        lds_flag_wr(rdy_addr, b);
+        if (seen_free < b + 1 - NS) {
+            seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+            if (seen_free < 0) return false;
+        }
+        return true;
+    };
+    // last wave: output row y = s0 + 3b + S - 2K, stored at voffset lane_off + (y - s0) * pitch
+    // of a buffer spanning the strip's rows: rows before s0 (negative offsets, as unsigned
+    // >= 2^32 - 2K * pitch) and from s1 on fall outside it, and so does a halo lane's 2^31.
+    const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
+        dst_b + (int64_t)s0 * pitch_b, (short)0, (int)(nrows * (uint32_t)pitch_b), 0x00020000);
+    uint32_t voff = st_off - (uint32_t)(2 * K) * (uint32_t)pitch_b;
+    const uint32_t strip_bytes = nrows * (uint32_t)pitch_b;
+    int rrel = -2 * K;  // output row - s0 (wave-uniform)
+    auto emit = [&](const uint32_t (&cur)[DW]) {
+        typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{cur[0], cur[1], cur[2], cur[3]}, strip_rs, voff, 0, GOL_ST_AUX);
+        // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are
+        // masked once at the end)
+        if (a.slots && (uint32_t)rrel < nrows)
+            alive += __popc(cur[0]) + __popc(cur[1]) + __popc(cur[2]) + __popc(cur[3]);
+        voff += (uint32_t)pitch_b;
+        ++rrel;
+    };
+    lds_u32 *const src_base = wv == 0 ? in_base : rd_base;
+    // block 0's row 0, read to completion here (the compiler copies the loop-carried register
+    // on loop entry, which must not happen while a read is in flight)
+    if (wv == 0) {
+        stage_in(0, in_ring[0]);
+        stage_in(1, in_ring[1]);
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else if (seen_ready < 1) {
+        seen_ready = spin_until_ge(ready_l + wv, 1);
+        if (seen_ready < 0) return;
+    }
+    v4u32 nextv = lds_rd128(src_base);
+    lds_flag_wr(wv == 0 ? scratch : cns_addr, 0);  // one younger LDS operation for block 0's wait
+    // ROLE 0 = loader (input from in_ring, staged from HBM), 1 = middle, 2 = last (stores)
+    auto step = [&](int b, auto u_c, auto role_c) -> bool {
+        constexpr int U = decltype(u_c)::value;
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool LAST = ROLE == 2;
+        uint32_t cur[DW];
+        auto realign = [&]() {
+            if (ROLE == 0 && wrap) {
+#pragma unroll
+                for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
+            }
+        };
+        // row 0
+        lds_wait_n<1>(nextv);  // younger: the consumed flag / scratch write, the previous row-2 write
+        unpack(nextv, cur);
+        nextv = lds_rd128_issue_o<U * SB + RB>(src_base);
+        realign();
+        compute(std::integral_constant<int, 0>(), cur);
+        if constexpr (LAST) {
+            emit(cur);
+        } else {
+            if (!publish_and_reserve(b)) return false;
+            lds_wr128_o<U * SB>(wr_base, pack(cur));
+        }
+        // row 1
+        lds_wait_n<LAST ? 0 : 1>(nextv);
+        unpack(nextv, cur);
+        nextv = lds_rd128_issue_o<U * SB + 2 * RB>(src_base);
+        realign();
+        compute(std::integral_constant<int, 1>(), cur);
+        if constexpr (LAST) emit(cur);
+        else lds_wr128_o<U * SB + RB>(wr_base, pack(cur));
+        // row 2; row 0 of block b+1 is read during it
+        lds_wait_n<LAST ? 0 : 1>(nextv);
+        unpack(nextv, cur);
+        if constexpr (ROLE == 0) {
+            stage_in(b + 2, in_ring[(U + 2) % 3]);               // refills block b-1's slot (clamped past the end)
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");     // block b+1 landed, b+2 in flight
+            nextv = lds_rd128_issue_o<((U + 1) % 3) * SB>(src_base);
+            lds_flag_wr(scratch, 0);
+        } else {
+            if (b + 1 < nblk3) {
+                if (seen_ready < b + 2) {
+                    seen_ready = spin_until_ge(ready_l + wv, b + 2);
+                    if (seen_ready < 0) return false;
+                }
+                nextv = lds_rd128_issue_o<((U + 1) % 3) * SB>(src_base);
+            }
+            lds_flag_wr(cns_addr, b + 1);
+        }
+        realign();
+        compute(std::integral_constant<int, 2>(), cur);
+        if constexpr (LAST) emit(cur);
+        else lds_wr128_o<U * SB + 2 * RB>(wr_base, pack(cur));
+        return true;
+    };
+    auto run = [&](auto role_c) {
+        for (int b = 0; b < nblk3; b += 3) {
+            if (!step(b, std::integral_constant<int, 0>(), role_c)) return;
+            if (!step(b + 1, std::integral_constant<int, 1>(), role_c)) return;
+            if (!step(b + 2, std::integral_constant<int, 2>(), role_c)) return;
+        }
+        if constexpr (decltype(role_c)::value != 2) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_flag_wr(rdy_addr, nblk3);
+        }
+    };
+    if (wv == 0) run(std::integral_constant<int, 0>());
+    else if (wv == P - 1) run(std::integral_constant<int, 2>());
+    else run(std::integral_constant<int, 1>());
+    alive &= st_mask;  // halo lanes' rows are not this group's
+    (void)strip_bytes;
+#elif GOL_PIPE_LGKM
     // One loop per role (0 = loader, 1 = middle, 2 = storer), so every LDS wait has a count
     // known at compile time.  Row S+1 is read while row S computes; a row wait lets the one
     // younger LDS operation (the previous row's ds_write) stay in flight instead of draining
@@ -1008,6 +1178,7 @@ band_pipe_kernel(BitsArgs a)
     auto role_loop = [&](auto role_c) {
         constexpr int ROLE = decltype(role_c)::value;
         constexpr bool WRITES = ROLE != 2;  // writes the next wave's ring
+        constexpr int ABL = GOL_PIPE_ABL;    // measurement-only ablations (wrong results)
         if constexpr (GOL_PIPE_PRIO == 1) __builtin_amdgcn_s_setprio(ROLE == 0 ? 3 : (ROLE == 1 ? 2 : 0));
         if constexpr (GOL_PIPE_PRIO == 2) __builtin_amdgcn_s_setprio(ROLE == 2 ? 3 : (ROLE == 1 ? 1 : 0));
         v4u32 nextv = fake;
@@ -1019,7 +1190,7 @@ band_pipe_kernel(BitsArgs a)
                 v4u32 v;
                 if (S == 0) {
                     PT_BEGIN();
-                    if (ROLE == 0) {
+                    if (ROLE == 0 && !(ABL & 4)) {
                         // block b landed; blocks b+1 .. b+NSI-2 (if any) may stay in flight
                         const int inflight = min(NSI - 2, nblk - 1 - b);
                         if (inflight >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
@@ -1027,11 +1198,13 @@ band_pipe_kernel(BitsArgs a)
                         else if (inflight == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
                         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
-                    if (ROLE != 0 && pre) {
+                    if (ABL & 2) {
+                        v = fake;
+                    } else if (ROLE != 0 && pre) {
                         lds_wait_n<1>(nextv);  // younger: the previous block's row 2 write / consumed flag
                         v = nextv;
                     } else {
-                        if (ROLE != 0 && seen_ready < b + 1) {
+                        if (ROLE != 0 && seen_ready < b + 1 && !(ABL & 1)) {
                             seen_ready = spin_until_ge(ready_l + wv, b + 1);
                             if (seen_ready < 0) { ok = false; return; }
                         }
@@ -1040,11 +1213,12 @@ band_pipe_kernel(BitsArgs a)
                     PT_END(pt_in);
                 } else {
                     PT_BEGIN();
-                    lds_wait_n<WRITES ? 1 : 0>(nextv);  // younger: row S-1's write
+                    if (!(ABL & 2)) lds_wait_n<WRITES ? 1 : 0>(nextv);  // younger: row S-1's write
                     PT_END(pt_lds);
-                    v = nextv;
+                    v = (ABL & 2) ? fake : nextv;
                 }
-                if (S < 2) {
+                if (ABL & 2) {
+                } else if (S < 2) {
                     nextv = lds_rd128_issue(slot_row(wv, b, S + 1));
                 } else {
                     pre = false;
@@ -1053,7 +1227,7 @@ band_pipe_kernel(BitsArgs a)
                         pre = true;
                     }
                     if (ROLE == 0) {
-                        if (b + NSI - 1 < nblk) stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);  // refills slot (b-1) % NSI
+                        if (!(ABL & 4) && b + NSI - 1 < nblk) stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);  // refills slot (b-1) % NSI
                     } else if (lane == 0) {
                         lds_wr32(consumed_l + wv, b + 1);
                     }
@@ -1077,7 +1251,7 @@ band_pipe_kernel(BitsArgs a)
                 }
                 if constexpr (!WRITES) {
                     const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                    store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
+                    if (!(ABL & 4)) store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
                     srow += pitch_b;
                     if (a.slots) {
                         uint32_t c = 0;
@@ -1091,14 +1265,15 @@ band_pipe_kernel(BitsArgs a)
                             lds_wait1();  // all but the row-1 read: block b-1's row writes are done
                             if (lane == 0) lds_wr32(ready_l + wv + 1, b);
                         }
-                        if (seen_free < b + 1 - NS) {  // slot b % NS of ring wv+1 free: block b-NS consumed
+                        if (seen_free < b + 1 - NS && !(ABL & 1)) {  // slot b % NS of ring wv+1 free: block b-NS consumed
                             PT_BEGIN();
                             seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
                             PT_END(pt_free);
                             if (seen_free < 0) { ok = false; return; }
                         }
                     }
-                    lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
+                    if (ABL & 2) fake = v4u32{cur[0], cur[1], cur[2], cur[3]} ^ fake;
+                    else lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
                 }
             }
         }
@@ -1208,6 +1383,7 @@ band_pipe_kernel(BitsArgs a)
     }
     return;
 #endif
+    if (GOL_PIPE_ABL & 2) alive += fake.x & fake.y & fake.z & fake.w & 1u;  // keep the ablated compute alive
     if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
 
@@ -1912,6 +2088,41 @@ int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
     return (int)strip;
 }
 
+// Workgroups of `kernel` (block threads) resident on the whole device at once (cached).
+static int64_t resident_workgroups(const void *kernel, int block)
+{
+    static std::mutex mu;
+    static std::map<const void *, int64_t> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(kernel);
+    if (it != cache.end()) return it->second;
+    int dev = 0, cus = 0, per_cu = 0;
+    int64_t n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) == hipSuccess)
+        n = (int64_t)cus * per_cu;
+    cache[kernel] = n;
+    return n;
+}
+
+// Strip length for a one-workgroup-per-(column group, strip) kernel on a board that fills
+// the device only a few times over: the strip count is a multiple of the strips that fit
+// in one round of resident workgroups, so the last round is not a small remainder (e.g.
+// 65536^2 at k = 12: 9 groups x 228 strips = 2052 workgroups was 2 rounds + 4 workgroups).
+// Boards of many rounds keep `fallback` (their tail is a small fraction already).
+static int64_t round_tiled_strip(int64_t rows, int64_t ngroups, int64_t slots, int64_t min_rows, int64_t cap,
+                                 int64_t fallback)
+{
+    if (slots <= 0 || rows <= 0) return fallback;
+    const int64_t per_round = std::max<int64_t>(1, slots / ngroups);
+    const int64_t rounds = (rows + per_round * cap - 1) / (per_round * cap);
+    if (rounds > 4) return fallback;
+    const int64_t nstrips = per_round * rounds;
+    const int64_t strip = (rows + nstrips - 1) / nstrips;
+    return std::min(rows, std::max(strip, min_rows));
+}
+
 hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
                           int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw,
                           int strip, uint64_t *slots, hipStream_t s)
@@ -1970,8 +2181,12 @@ static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s
 }
 
 template <int KW, int P>
-static hipError_t launch_band_split(bool contig, const BitsArgs &a, hipStream_t s)
+static hipError_t launch_band_split(bool contig, BitsArgs a, hipStream_t s, bool auto_strip = false)
 {
+    if (auto_strip) {
+        const void *kf = contig ? (const void *)band_pipe_kernel<KW, P, true> : (const void *)band_pipe_kernel<KW, P, false>;
+        a.strip = (int)round_tiled_strip(a.rows, a.ngroups, resident_workgroups(kf, 64 * P), 8 * KW * P, 1024, a.strip);
+    }
     const dim3 grid(a.ngroups, (int)((a.rows + a.strip - 1) / a.strip));
     static const int sync = [] {  // 1 = LDS flags (default), 0 = one workgroup barrier per block
         const char *e = getenv("GOL_SPLIT_SYNC");
@@ -2043,6 +2258,9 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
         // one workgroup per (column group, strip): strips up to 1024 rows (measured best at k = 12)
         a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP)
                             : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(1024, rows * a.ngroups / 2048)));
+        // the pipe kernel's stores address a strip as one buffer (32-bit range)
+        a.strip = (int)std::max<int64_t>(1, std::min<int64_t>(a.strip, (int64_t(1) << 30) / (pitch * 4)));
+        const bool auto_strip = strip <= 0;
         a.slots = slots;
         const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
         if (k == 8) return launch_band_split<GOL_SPLIT_KW == 4 ? 4 : 2, GOL_SPLIT_KW == 4 ? 2 : 4>(contig, a, s);
@@ -2052,11 +2270,10 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
                 const char *e = getenv("GOL_PIPE_WAVES");
                 return e ? atoi(e) : 12 / GOL_SPLIT_KW;
             }();
-            if (shape == 3) return launch_band_split<4, 3>(contig, a, s);
-            if (shape == 2) return launch_band_split<6, 2>(contig, a, s);
-            return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s);
+            if (shape == 3) return launch_band_split<4, 3>(contig, a, s, auto_strip);
+            return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s, auto_strip);
         }
-        if (k == 24) return launch_band_split<3, 8>(contig, a, s);  // 8 waves x 3 stages
+        if (k == 24) return launch_band_split<3, 8>(contig, a, s, auto_strip);  // 8 waves x 3 stages
         return launch_band_split<4, 4>(contig, a, s);
     }
     BitsArgs a;
@@ -2132,7 +2349,11 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
     }();
     if (k == 32 || (k == 16 && bpipe)) {
         // one workgroup of k/4 waves per (column group, strip); strips >= 8k rows
-        if (strip <= 0) a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
+        if (strip <= 0) {
+            a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
+            const void *kf = k == 32 ? (const void *)bytes_pipe_kernel<4, 8> : (const void *)bytes_pipe_kernel<4, 4>;
+            a.strip = (int)round_tiled_strip(rows, a.ngroups, resident_workgroups(kf, 16 * k), 8 * k, 1024, a.strip);
+        }
         const dim3 g2(a.ngroups, (int)((rows + a.strip - 1) / a.strip));
         if (k == 32) hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), g2, dim3(512), 0, s, a);
         else hipLaunchKernelGGL((bytes_pipe_kernel<4, 4>), g2, dim3(256), 0, s, a);

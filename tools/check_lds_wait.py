@@ -47,7 +47,7 @@ def kernels(asm, pattern):
         name = m.group(1)
         if not re.search(pattern, name):
             continue
-        end = asm.find("s_endpgm", m.end())
+        end = asm.find(".Lfunc_end", m.end())  # the whole function: a kernel may have several s_endpgm
         yield name, asm[m.end():end]
 
 
