@@ -8,6 +8,8 @@ Workloads (a "step" = one pass of the hot path = one k-turn launch over the boar
   weak     (default) bit-packed torus of 2^17 rows x 2^20 columns PER GPU, rows sharded
            over the ranks with a k-row RCCL halo exchange (SURVEY.md §8(d) weak-scaling
            config; N = 8 is the 2^20 x 2^20 torus of BASELINE.json config 5).
+  strong262k  262144 x 262144 bit-packed torus, rows sharded over the N ranks (config 4:
+           total work fixed as N grows, "scaling": "strong").
   bit64k   65536 x 65536 bit-packed torus on one GPU (config 3); replicas for N > 1.
   byte16k  16384 x 16384 byte-per-cell torus, 1 turn per step (config 2); replicas for N > 1.
 
@@ -40,7 +42,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="weak", choices=["weak", "bit64k", "byte16k"])
+    ap.add_argument("--workload", default="weak", choices=["weak", "strong262k", "bit64k", "byte16k"])
     ap.add_argument("--k", type=int, default=0,
                     help="turns per launch (temporal blocking); 0 = library default for bit boards "
                          "(12 band / 8 standard), 32 for byte16k")
@@ -54,6 +56,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample length")
     ap.add_argument("--no-count", action="store_true",
                     help="do not fuse the alive-cell count (AliveCellsCount) into every launch")
+    ap.add_argument("--snapshot-rows", type=int, default=0,
+                    help="after the timed steps, stream this many board rows per rank as P5 bytes "
+                         "(device unpack -> host, golhip.sharded.stream_pgm's path) and report the rate "
+                         "(config 5's PGM snapshot; not part of value)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="testing only: every rank uses cuda:0 (multi-rank logic on a 1-GPU box, with --backend gloo)")
@@ -152,6 +158,8 @@ def run_bits(args, rank, world):
     from golhip.sharded import ShardedBoard
     if args.workload == "weak":
         H, W, nshards = args.rows_per_gpu * world, args.width, world
+    elif args.workload == "strong262k":
+        H, W, nshards = 262144, 262144, world
     else:
         H, W, nshards = 65536, 65536, 1
     group = None
@@ -202,11 +210,34 @@ def run_bits(args, rank, world):
     rpg = args.rows_per_gpu
     rows_name = f"2^{rpg.bit_length() - 1}" if rpg & (rpg - 1) == 0 else str(rpg)
     wname = f"2^{W.bit_length() - 1}" if W & (W - 1) == 0 else str(W)
-    cfg = {"workload": (f"weak-{rows_name}x{wname}-per-gpu" if args.workload == "weak" else "bit-65536x65536"),
+    snap = snapshot(board, args.snapshot_rows, world) if args.snapshot_rows > 0 else None
+    name = {"weak": f"weak-{rows_name}x{wname}-per-gpu", "strong262k": "strong-262144x262144",
+            "bit64k": "bit-65536x65536"}[args.workload]
+    cfg = {"workload": name,
            "H": H, "W": W, "parallelism": (f"rows{world}" if nshards > 1 else (f"replicas{world}" if world > 1 else "1gpu")),
            **info}
+    if snap is not None:
+        cfg["snapshot"] = snap
     dtype = "u32 (bit-packed, 32 cells/word" + (", column-band layout)" if layout == "band" else ")")
     return value, dt, cfg, roof, dtype
+
+
+def snapshot(board, rows, world):
+    """Config 5's PGM snapshot path, bounded: every rank unpacks its first `rows` rows on the GPU
+    (bits -> 0/255 bytes, golhip.sharded.stream_pgm's chunked path) and copies them to the host;
+    reported as host bytes/s over all ranks (PCIe-inclusive, not part of value)."""
+    rows = min(rows, board.R)
+    std = board.standard()
+    chunk = 4096
+    barrier(world)
+    t0 = time.perf_counter()
+    n = 0
+    for a in range(0, rows, chunk):
+        part = board.kern.unpack(std[a:a + min(chunk, rows - a)], board.W)
+        n += part.cpu().numpy().nbytes
+    torch.cuda.synchronize()
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    return {"rows_per_rank": rows, "bytes": n * world, "GB_per_s": round(n * world / dt / 1e9, 2)}
 
 
 def run_bytes(args, rank, world):
@@ -285,7 +316,8 @@ def main():
         line = {"metric": "cell-updates/sec (GCUPS) + % HBM roofline", "value": round(value / 1e9, 2),
                 "unit": "GCUPS", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+                "scaling": "strong" if args.workload == "strong262k" else "weak", "vs_baseline": None,
+                "dtype": dtype,
                 "data": "synthetic (splitmix64 Bernoulli(1/2) torus generated on the GPU)",
                 "config": cfg, "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)

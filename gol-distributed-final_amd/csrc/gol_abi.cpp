@@ -443,19 +443,16 @@ extern "C" int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t strid
     return GOL_OK;
 }
 
-extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
+// Row-major (x, y) list of the cells of `board` that are alive (prev == NULL) or whose alive
+// state differs from `prev`: per-row counts -> host exclusive scan -> one wave per row.
+static int list_cells(gol_engine *e, bool bm, const void *board, const void *prev, int64_t units, int64_t pitch,
+                      int32_t *xy, int64_t cap, int64_t *n, const char *what)
 {
-    if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
-    int rc = engine_dev(e);
-    if (rc || (rc = ensure_standard(e))) return rc;
-    const bool bm = e->bit_mode;
-    const void *board = bm ? (const void *)e->bits[e->cur] : (const void *)e->bytes[e->bcur];
-    const int64_t units = bm ? e->Wd : e->W, pitch = bm ? e->pitch : e->bstride;
     int64_t *dcounts = nullptr;
     int32_t *dxy = nullptr;
     std::vector<int64_t> counts(e->H);
     HIPCHK(hipMalloc(&dcounts, e->H * sizeof(int64_t)));
-    hipError_t he = golk_row_counts(bm, board, e->H, units, pitch, dcounts, e->stream);
+    hipError_t he = golk_row_counts(bm, board, prev, e->H, units, pitch, dcounts, e->stream);
     if (he == hipSuccess)
         he = hipMemcpyAsync(counts.data(), dcounts, e->H * sizeof(int64_t), hipMemcpyDeviceToHost, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
@@ -472,15 +469,64 @@ extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, i
     if (he == hipSuccess && m > 0) {
         he = hipMemcpyAsync(dcounts, counts.data(), e->H * sizeof(int64_t), hipMemcpyHostToDevice, e->stream);
         if (he == hipSuccess) he = hipMalloc(&dxy, m * 2 * sizeof(int32_t));
-        if (he == hipSuccess) he = golk_alive_list(bm, board, e->H, units, pitch, dcounts, dxy, m, e->stream);
+        if (he == hipSuccess)
+            he = golk_alive_list(bm, board, prev, e->H, units, pitch, dcounts, dxy, m, e->stream);
         if (he == hipSuccess)
             he = hipMemcpyAsync(xy, dxy, m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
         if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     }
     (void)hipFree(dcounts);
     if (dxy) (void)hipFree(dxy);
-    if (he != hipSuccess) return gol_set_error(GOL_EHIP, "alive_cells: %s", hipGetErrorString(he));
+    if (he != hipSuccess) return gol_set_error(GOL_EHIP, "%s: %s", what, hipGetErrorString(he));
     return GOL_OK;
+}
+
+extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
+{
+    if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
+    int rc = engine_dev(e);
+    if (rc || (rc = ensure_standard(e))) return rc;
+    const bool bm = e->bit_mode;
+    const void *board = bm ? (const void *)e->bits[e->cur] : (const void *)e->bytes[e->bcur];
+    return list_cells(e, bm, board, nullptr, bm ? e->Wd : e->W, bm ? e->pitch : e->bstride, xy, cap, n,
+                      "alive_cells");
+}
+
+extern "C" int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
+{
+    if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
+    int rc = engine_dev(e);
+    if (rc || (rc = ensure_standard(e))) return rc;
+    if (e->bit_mode) {
+        // one standard-layout turn; the previous generation stays in the other buffer
+        const uint32_t *mid = e->bits[e->cur];
+        HIPCHK(golk_bits_step(mid + (e->H - 1) * e->pitch, mid, mid, e->bits[1 - e->cur], e->H, e->Wd, e->pitch, 0,
+                              e->H, 1, e->dw, e->strip, nullptr, e->stream));
+        e->cur = 1 - e->cur;
+        e->turn += 1;
+        return list_cells(e, true, e->bits[e->cur], e->bits[1 - e->cur], e->Wd, e->pitch, xy, cap, n,
+                          "step_flips");
+    }
+    // byte board (loaded bytes other than 0/255, or W % 64 != 0): keep the previous bytes; the
+    // turn may move the board to the bit board, whose bytes are unpacked for the comparison
+    uint8_t *prev = nullptr, *now = nullptr;
+    HIPCHK(hipMalloc(&prev, e->H * e->bstride));
+    hipError_t he = hipMemcpyAsync(prev, e->bytes[e->bcur], e->H * e->bstride, hipMemcpyDeviceToDevice, e->stream);
+    if (he == hipSuccess && (rc = gol_engine_step_async(e, 1, nullptr)) == GOL_OK) {
+        const uint8_t *cur = e->bit_mode ? nullptr : e->bytes[e->bcur];
+        if (e->bit_mode) {
+            he = hipMalloc(&now, e->H * e->bstride);
+            if (he == hipSuccess)
+                he = golk_unpack(e->bits[e->cur], e->H, e->W, e->pitch, now, e->bstride, e->stream);
+            cur = now;
+        }
+        if (he == hipSuccess) rc = list_cells(e, false, cur, prev, e->W, e->bstride, xy, cap, n, "step_flips");
+    }
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    (void)hipFree(prev);
+    if (now) (void)hipFree(now);
+    if (rc == GOL_OK && he != hipSuccess) rc = gol_set_error(GOL_EHIP, "step_flips: %s", hipGetErrorString(he));
+    return rc;
 }
 
 extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)

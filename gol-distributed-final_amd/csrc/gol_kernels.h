@@ -50,7 +50,9 @@ hipError_t golk_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stri
                      uint32_t *nonbinary, hipStream_t s);
 hipError_t golk_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes, int64_t stride,
                        hipStream_t s);
-hipError_t golk_row_counts(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
-                           int64_t *out, hipStream_t s);
-hipError_t golk_alive_list(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
-                           const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s);
+// Per-row counts and the row-major (x, y) list of alive cells; with prev != NULL of the cells
+// whose alive state differs between board and prev (same layout and pitch).
+hipError_t golk_row_counts(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
+                           int64_t pitch, int64_t *out, hipStream_t s);
+hipError_t golk_alive_list(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
+                           int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s);

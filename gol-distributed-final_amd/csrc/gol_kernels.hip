@@ -1951,8 +1951,10 @@ __global__ void unpack_kernel(const uint32_t *bits, int64_t rows, int64_t W, int
 
 // Alive-cell list, row-major (broker.go:47-58): one wave per row, ballot + mbcnt
 // prefix over 64 cells at a time.  offs[y] = first output index of row y.
-__global__ void alive_list_bits_kernel(const uint32_t *bits, int64_t rows, int64_t Wd, int64_t pitch,
-                                       const int64_t *offs, int32_t *xy, int64_t cap)
+// With `prev` the listed cells are those that differ from `prev` (the CellFlipped events of
+// one turn, gol/event.go:50-60): the same kernels over bits ^ prev.
+__global__ void alive_list_bits_kernel(const uint32_t *bits, const uint32_t *prev, int64_t rows, int64_t Wd,
+                                       int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap)
 {
     const int lane = threadIdx.x & 63;
     const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1960,7 +1962,7 @@ __global__ void alive_list_bits_kernel(const uint32_t *bits, int64_t rows, int64
     int64_t base = offs[y];
     for (int64_t w0 = 0; w0 < Wd; w0 += 64) {
         const int64_t w = w0 + lane;
-        const uint32_t v = w < Wd ? bits[y * pitch + w] : 0u;
+        const uint32_t v = w < Wd ? bits[y * pitch + w] ^ (prev ? prev[y * pitch + w] : 0u) : 0u;
         const uint32_t c = __popc(v);
         // exclusive prefix of c over the wave
         uint32_t incl = c;
@@ -1981,8 +1983,15 @@ __global__ void alive_list_bits_kernel(const uint32_t *bits, int64_t rows, int64
     }
 }
 
-__global__ void alive_list_bytes_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride,
-                                        const int64_t *offs, int32_t *xy, int64_t cap)
+// bytes: a cell is alive when != 0 (broker.go:50-55); with `prev`, listed when its alive state
+// differs from prev's.
+__device__ __forceinline__ bool byte_listed(const uint8_t *bytes, const uint8_t *prev, int64_t i)
+{
+    return (bytes[i] != 0) != (prev ? prev[i] != 0 : false);
+}
+
+__global__ void alive_list_bytes_kernel(const uint8_t *bytes, const uint8_t *prev, int64_t rows, int64_t W,
+                                        int64_t stride, const int64_t *offs, int32_t *xy, int64_t cap)
 {
     const int lane = threadIdx.x & 63;
     const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1990,7 +1999,7 @@ __global__ void alive_list_bytes_kernel(const uint8_t *bytes, int64_t rows, int6
     int64_t base = offs[y];
     for (int64_t x0 = 0; x0 < W; x0 += 64) {
         const int64_t x = x0 + lane;
-        const bool alive = x < W && bytes[y * stride + x] != 0;
+        const bool alive = x < W && byte_listed(bytes, prev, y * stride + x);
         const uint64_t m = __ballot(alive);
         if (alive) {
             const int64_t o = base + __popcll(m & ((1ULL << lane) - 1));
@@ -2000,24 +2009,26 @@ __global__ void alive_list_bytes_kernel(const uint8_t *bytes, int64_t rows, int6
     }
 }
 
-__global__ void row_counts_bits_kernel(const uint32_t *bits, int64_t rows, int64_t Wd, int64_t pitch, int64_t *out)
+__global__ void row_counts_bits_kernel(const uint32_t *bits, const uint32_t *prev, int64_t rows, int64_t Wd,
+                                       int64_t pitch, int64_t *out)
 {
     const int lane = threadIdx.x & 63;
     const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
     if (y >= rows) return;
     uint64_t c = 0;
-    for (int64_t w = lane; w < Wd; w += 64) c += __popc(bits[y * pitch + w]);
+    for (int64_t w = lane; w < Wd; w += 64) c += __popc(bits[y * pitch + w] ^ (prev ? prev[y * pitch + w] : 0u));
     c = wave_sum_u64(c);
     if (lane == 0) out[y] = (int64_t)c;
 }
 
-__global__ void row_counts_bytes_kernel(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, int64_t *out)
+__global__ void row_counts_bytes_kernel(const uint8_t *bytes, const uint8_t *prev, int64_t rows, int64_t W,
+                                        int64_t stride, int64_t *out)
 {
     const int lane = threadIdx.x & 63;
     const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
     if (y >= rows) return;
     uint64_t c = 0;
-    for (int64_t x = lane; x < W; x += 64) c += bytes[y * stride + x] != 0;
+    for (int64_t x = lane; x < W; x += 64) c += byte_listed(bytes, prev, y * stride + x);
     c = wave_sum_u64(c);
     if (lane == 0) out[y] = (int64_t)c;
 }
@@ -2425,30 +2436,30 @@ hipError_t golk_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pi
     return hipGetLastError();
 }
 
-hipError_t golk_row_counts(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
-                           int64_t *out, hipStream_t s)
+hipError_t golk_row_counts(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
+                           int64_t pitch, int64_t *out, hipStream_t s)
 {
     const int wpb = 4;
     dim3 grid((unsigned)((rows + wpb - 1) / wpb));
     if (bits_mode)
-        hipLaunchKernelGGL(row_counts_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board, rows,
-                           width_units, pitch, out);
+        hipLaunchKernelGGL(row_counts_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board,
+                           (const uint32_t *)prev, rows, width_units, pitch, out);
     else
-        hipLaunchKernelGGL(row_counts_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board, rows,
-                           width_units, pitch, out);
+        hipLaunchKernelGGL(row_counts_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board,
+                           (const uint8_t *)prev, rows, width_units, pitch, out);
     return hipGetLastError();
 }
 
-hipError_t golk_alive_list(bool bits_mode, const void *board, int64_t rows, int64_t width_units, int64_t pitch,
-                           const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s)
+hipError_t golk_alive_list(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
+                           int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s)
 {
     const int wpb = 4;
     dim3 grid((unsigned)((rows + wpb - 1) / wpb));
     if (bits_mode)
-        hipLaunchKernelGGL(alive_list_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board, rows,
-                           width_units, pitch, offs, xy, cap);
+        hipLaunchKernelGGL(alive_list_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board,
+                           (const uint32_t *)prev, rows, width_units, pitch, offs, xy, cap);
     else
-        hipLaunchKernelGGL(alive_list_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board, rows,
-                           width_units, pitch, offs, xy, cap);
+        hipLaunchKernelGGL(alive_list_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board,
+                           (const uint8_t *)prev, rows, width_units, pitch, offs, xy, cap);
     return hipGetLastError();
 }

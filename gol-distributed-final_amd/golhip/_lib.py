@@ -80,6 +80,7 @@ SIGNATURES = [
     ("gol_engine_alive_count", ctypes.c_int, [_vp, _P(_u64)]),
     ("gol_engine_store_bytes", ctypes.c_int, [_vp, _vp, _i64]),
     ("gol_engine_alive_cells", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
+    ("gol_engine_step_flips", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
     ("gol_engine_write_pgm", ctypes.c_int, [_vp, ctypes.c_char_p]),
     ("gol_engine_hash", ctypes.c_int, [_vp, _P(_u64)]),
     ("gol_engine_info", ctypes.c_int, [_vp, _P(_i32), _P(_i32), _P(_i32), _P(_i32)]),

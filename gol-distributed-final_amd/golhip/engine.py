@@ -83,6 +83,16 @@ class Engine:
         check(lib().gol_engine_alive_cells(self._h, xy.ctypes.data, cap, ctypes.byref(n)))
         return xy[:min(n.value, cap)]
 
+    def step_flips(self, cap: int | None = None) -> np.ndarray:
+        """Advance one turn; (n, 2) int32 (x, y) of the cells that changed, row-major: the
+        CellFlipped events of that turn (gol/event.go:50-60)."""
+        if cap is None:
+            cap = self.H * self.W
+        xy = np.zeros((max(cap, 1), 2), dtype=np.int32)
+        n = ctypes.c_int64()
+        check(lib().gol_engine_step_flips(self._h, xy.ctypes.data, cap, ctypes.byref(n)))
+        return xy[:min(n.value, cap)]
+
     def hash(self) -> int:
         h = ctypes.c_uint64()
         check(lib().gol_engine_hash(self._h, ctypes.byref(h)))

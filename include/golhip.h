@@ -114,6 +114,12 @@ int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t stride);
 /* calculateAliveCells (broker.go:47-58): (x, y) int32 pairs in row-major
  * order; writes min(n, cap) pairs, *n = total alive cells. */
 int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n);
+/* Advance exactly one turn and list the cells whose state changed, (x, y) int32
+ * pairs in row-major order: the CellFlipped{CompletedTurns, Cell} events of
+ * that turn (gol/event.go:50-60; sent per flipped cell by the controller the
+ * reference never finished, README.md:260-262).  Writes min(n, cap) pairs,
+ * *n = number of flipped cells. */
+int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n);
 /* writePgmImage byte stream (gol/io.go:52-81): "P5\n<W> <H>\n255\n" + H*W
  * bytes, streamed from the device in chunks. */
 int gol_engine_write_pgm(gol_engine *e, const char *path);

@@ -123,6 +123,14 @@ def alive_cells(world: np.ndarray) -> list[tuple[int, int]]:
     return [(int(xy[2 * i]), int(xy[2 * i + 1])) for i in range(n)]
 
 
+def flipped_cells(prev: np.ndarray, cur: np.ndarray) -> list[tuple[int, int]]:
+    """CellFlipped events of one turn (gol/event.go:50-60: one event per cell whose state
+    changed between CompletedTurns-1 and CompletedTurns), row-major [(X, Y)] like
+    calculateAliveCells (broker.go:47-58); alive = byte != 0."""
+    ys, xs = np.nonzero((np.asarray(prev) != 0) != (np.asarray(cur) != 0))
+    return list(zip(xs.tolist(), ys.tolist()))
+
+
 # ---------------------------------------------------------------- numpy restatement
 def np_next_state(world: np.ndarray) -> np.ndarray:
     """Same rule as worker.go:15-70, vectorised: count of ==255 neighbours on

@@ -482,3 +482,59 @@ def test_byte_pipe_k16_switch(golhip):
     r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "GOL_BYTES_PIPE16": "1"},
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+# ------------------------------------------------------------------ CellFlipped stream
+def _check_flips(e, board, turns):
+    """step_flips() per turn == oracle diff of consecutive generations; replaying the flips
+    onto the previous board gives the new one (what an SDL view does, sdl/loop.go:9-53)."""
+    prev = board
+    shown = (board != 0).astype(np.uint8)
+    for t in range(1, turns + 1):
+        got = [tuple(c) for c in e.step_flips().tolist()]
+        cur = O.run(board, t)
+        assert got == O.flipped_cells(prev, cur), f"turn {t}"
+        for x, y in got:
+            shown[y, x] ^= 1
+        assert np.array_equal(shown, (cur != 0).astype(np.uint8))
+        assert e.turn == t
+        prev = cur
+    assert np.array_equal(e.store_bytes(), prev)
+
+
+def test_step_flips_golden_board(golhip, golden_dir):
+    board = _golden_board(golden_dir, 64)
+    with golhip.Engine(64, 64, device=0) as e:
+        e.load_bytes(board)
+        _check_flips(e, board, 12)
+
+
+@pytest.mark.parametrize("shape", [(130, 1024), (33, 48), (40, 96)])
+def test_step_flips_layouts(golhip, shape):
+    """Band-capable width (after k-turn band steps), a byte-only width and a standard one."""
+    H, W = shape
+    rng = np.random.default_rng(H + W)
+    board = (rng.random((H, W)) < 0.35).astype(np.uint8) * 255
+    with golhip.Engine(H, W, device=0) as e:
+        e.load_bytes(board)
+        e.step(12)
+        start = O.run(board, 12)
+        prev = start
+        for t in range(1, 4):
+            got = [tuple(c) for c in e.step_flips().tolist()]
+            cur = O.run(start, t)
+            assert got == O.flipped_cells(prev, cur)
+            prev = cur
+        assert e.turn == 15
+        part = e.step_flips(cap=5)
+        assert [tuple(c) for c in part.tolist()] == O.flipped_cells(prev, O.run(start, 4))[:5]
+
+
+def test_step_flips_non_binary_first_turn(golhip):
+    """Turn 1 from bytes other than 0/255: a non-zero byte that dies is a flip (alive = != 0)."""
+    rng = np.random.default_rng(11)
+    for H, W in [(64, 128), (33, 48)]:
+        board = rng.choice(np.array([0, 255, 1, 7, 128], dtype=np.uint8), size=(H, W), p=[.5, .35, .05, .05, .05])
+        with golhip.Engine(H, W, device=0) as e:
+            e.load_bytes(board)
+            _check_flips(e, board, 3)
