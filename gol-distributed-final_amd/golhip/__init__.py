@@ -4,6 +4,7 @@
 * ``Operations``           broker RPC service mirror (broker.go:62-277)
 * ``GameOfLifeOperations`` worker RPC service mirror (worker.go:73-86)
 * ``ShardedBoard``         row-sharded torus, one process per GPU, RCCL halo exchange
+* ``distributor``          controller mirror (gol/gol.go + gol/distributor.go) over the broker API
 * ``next_state_slab`` / ``partition_rows``  worker.go:15-70 / broker.go:135-206
 
 Everything runs through libgolhip.so (hipcc, gfx950); there is no CPU fallback.
