@@ -313,7 +313,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, cfg["H"], cfg["W"], cfg.get("turns_per_step", 1))
     if rank == 0:
-        line = {"metric": "cell-updates/sec (GCUPS) + % HBM roofline", "value": round(value / 1e9, 2),
+        line = {"metric": "cell-updates/sec (GCUPS) + % HBM roofline at 1/2/4/8 MI355X", "value": round(value / 1e9, 2),
                 "unit": "GCUPS", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
                 "scaling": "strong" if args.workload == "strong262k" else "weak", "vs_baseline": None,

@@ -132,3 +132,37 @@ def test_sharded_gpu_load_pgm_band(tmp_path):
     res = _run_pgm(3, str(p), W, H, turns)
     ref = O.unpack(O.bits_run(O.pack(board), turns))
     assert np.array_equal(res[0][1], ref)
+
+
+def _bench_line(args, nproc, port):
+    """Run bench.py (1 rank, or `nproc` ranks under torch.distributed.run) and parse its JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if nproc == 1:
+        cmd = [sys.executable, "bench.py"] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py",
+               "--gpus", str(nproc), "--backend", "gloo", "--share-gpu"] + args
+    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_match_one_rank():
+    """bench.py's N > 1 path (barrier, max-over-ranks timing, sharded weak board, fused count):
+    2 ranks x 2048 rows give the same alive count as 1 rank x 4096 rows of the same torus
+    (the synthetic board is a function of the global row), and the line reports the whole job."""
+    common = ["--width", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    two = _bench_line(["--rows-per-gpu", "2048"] + common, 2, _free_port())
+    one = _bench_line(["--rows-per-gpu", "4096"] + common, 1, 0)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["H"] == one["config"]["H"] == 4096
+    assert two["config"]["turns_done"] == one["config"]["turns_done"]
+    assert two["config"]["alive_final"] == one["config"]["alive_final"]
+    k = one["config"]["turns_per_step"]
+    assert abs(two["value"] - 4096 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
