@@ -1592,6 +1592,9 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
         : "memory");
 }
 
+#ifndef GOL_BYTES_PIPE_DEFER
+#define GOL_BYTES_PIPE_DEFER 1  // +2.8 % on byte16k (same-box A/B, profiles/r01_final/ab_defer.log)
+#endif
 template <int KW, int P>
 __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 {
@@ -1680,6 +1683,43 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
             lds_rd32x3(slot_row(wv, b, 0), rows3);
             if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
         }
+#if GOL_BYTES_PIPE_DEFER
+        // the three rows' stages first, one basic block the scheduler can interleave (stage g
+        // of row S+1 is independent of stage g+1 of row S), then the stores / ring writes
+        uint32_t outw[3];
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+            uint32_t cur[1];
+            if (wv == 0) cur[0] = pack32(buf[PAR][S].lo, buf[PAR][S].hi);
+            else cur[0] = rows3[S];
+#pragma unroll
+            for (int g = 0; g < KW; ++g) {
+                if (S == 0) PS::template stage<0>(p, g, cur);
+                if (S == 1) PS::template stage<1>(p, g, cur);
+                if (S == 2) PS::template stage<2>(p, g, cur);
+            }
+            outw[S] = cur[0];
+        }
+        if (wv == P - 1) {
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+                const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
+                const uint32_t nx = from_upper_lane(outw[S]);
+                const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, outw[S], K % 32) : nx;
+                store(srow, row_ok ? row_bytes : 0u, o);
+                srow += pitch;
+                if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
+            }
+        } else {
+            if (seen_free < b + 1 - NS) {
+                seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                ok = seen_free >= 0;
+                if (!ok) return;
+            }
+#pragma unroll
+            for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)outw[S]);
+        }
+#else
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[1];
@@ -1709,6 +1749,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                 lds_wr32(slot_row(wv + 1, b, S), (int)cur[0]);
             }
         }
+#endif
         if (wv < P - 1) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
