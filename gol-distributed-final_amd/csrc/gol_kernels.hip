@@ -1595,8 +1595,15 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
 #ifndef GOL_BYTES_PIPE_DEFER
 #define GOL_BYTES_PIPE_DEFER 1  // +2.8 % on byte16k (same-box A/B, profiles/r01_final/ab_defer.log)
 #endif
+#ifndef GOL_BYTES_PIPE_WPE
+#define GOL_BYTES_PIPE_WPE 0  // > 0: waves per SIMD the compiler must fit (occupancy experiment)
+#endif
 template <int KW, int P>
-__global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
+__global__ void __launch_bounds__(64 * P)
+#if GOL_BYTES_PIPE_WPE > 0
+__attribute__((amdgpu_waves_per_eu(GOL_BYTES_PIPE_WPE)))
+#endif
+bytes_pipe_kernel(BytesKArgs a)
 {
     constexpr int K = KW * P;
     static_assert(K <= 32, "one 32-cell halo word per side");
