@@ -1595,6 +1595,9 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
 #ifndef GOL_BYTES_PIPE_DEFER
 #define GOL_BYTES_PIPE_DEFER 1  // +2.8 % on byte16k (same-box A/B, profiles/r01_final/ab_defer.log)
 #endif
+#ifndef GOL_BYTES_PIPE_NB
+#define GOL_BYTES_PIPE_NB 1  // loader's raw byte blocks in registers (1: 67 VGPRs, 3 workgroups per CU; +13 % on byte16k)
+#endif
 #ifndef GOL_BYTES_PIPE_WPE
 #define GOL_BYTES_PIPE_WPE 0  // > 0: waves per SIMD the compiler must fit (occupancy experiment)
 #endif
@@ -1661,8 +1664,10 @@ bytes_pipe_kernel(BytesKArgs a)
     typedef PipeSel<KW, 1, 1> PS;
     typename PS::type p;
     PS::init(p);
-    // wave 0: raw bytes of the current and the next block in registers (8 VGPRs per row)
-    Raw32 buf[2][3];
+    // wave 0: raw bytes of the current and the next block in registers (8 VGPRs per row);
+    // NB = 1: one block, packed before the next block's loads are issued into it
+    constexpr int NB = GOL_BYTES_PIPE_NB;
+    Raw32 buf[NB][3];
     if (wv == 0) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) load(first_in + s, buf[0][s]);
@@ -1674,9 +1679,14 @@ bytes_pipe_kernel(BytesKArgs a)
     char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch;
     auto block = [&](int b, auto par) {
         constexpr int PAR = decltype(par)::value;  // wave 0's buffer of block b
+        uint32_t rows3[3] = {0, 0, 0};
         if (wv == 0) {
+            if constexpr (NB == 1) {
 #pragma unroll
-            for (int s = 0; s < 3; ++s) load(first_in + 3 * (b + 1) + s, buf[1 - PAR][s]);  // clamped past the end
+                for (int s = 0; s < 3; ++s) rows3[s] = pack32(buf[0][s].lo, buf[0][s].hi);
+            }
+#pragma unroll
+            for (int s = 0; s < 3; ++s) load(first_in + 3 * (b + 1) + s, buf[(1 - PAR) % NB][s]);  // clamped past the end
         } else if (seen_ready < b + 1) {
             seen_ready = spin_until_ge(ready_l + wv, b + 1);
             ok = seen_ready >= 0;
@@ -1685,7 +1695,6 @@ bytes_pipe_kernel(BytesKArgs a)
         // the block's three rows, read and waited for in one asm statement: a split issue /
         // wait lets the compiler copy the destination VGPR while the read is in flight (it did
         // here; tools/check_lds_wait.py scans the assembly for that)
-        uint32_t rows3[3] = {0, 0, 0};
         if (wv != 0) {
             lds_rd32x3(slot_row(wv, b, 0), rows3);
             if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
@@ -1697,7 +1706,7 @@ bytes_pipe_kernel(BytesKArgs a)
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[1];
-            if (wv == 0) cur[0] = pack32(buf[PAR][S].lo, buf[PAR][S].hi);
+            if (wv == 0 && NB == 2) cur[0] = pack32(buf[PAR % NB][S].lo, buf[PAR % NB][S].hi);
             else cur[0] = rows3[S];
 #pragma unroll
             for (int g = 0; g < KW; ++g) {
@@ -1730,7 +1739,7 @@ bytes_pipe_kernel(BytesKArgs a)
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             uint32_t cur[1];
-            if (wv == 0) cur[0] = pack32(buf[PAR][S].lo, buf[PAR][S].hi);
+            if (wv == 0 && NB == 2) cur[0] = pack32(buf[PAR % NB][S].lo, buf[PAR % NB][S].hi);
             else cur[0] = rows3[S];
 #pragma unroll
             for (int g = 0; g < KW; ++g) {
@@ -2411,7 +2420,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         if (strip <= 0) {
             a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
             const void *kf = k == 32 ? (const void *)bytes_pipe_kernel<4, 8> : (const void *)bytes_pipe_kernel<4, 4>;
-            a.strip = (int)round_tiled_strip(rows, a.ngroups, resident_workgroups(kf, 16 * k), 8 * k, 1024, a.strip);
+            a.strip = (int)round_tiled_strip(rows, a.ngroups, resident_workgroups(kf, 16 * k), 4 * k, 1024, a.strip);
         }
         const dim3 g2(a.ngroups, (int)((rows + a.strip - 1) / a.strip));
         if (k == 32) hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), g2, dim3(512), 0, s, a);
