@@ -1,26 +1,34 @@
 """Benchmark of the Game-of-Life hot path on MI355X (BASELINE.json metric:
-cell-updates/s (GCUPS) and % of the HBM roofline at 1/2/4/8 GPUs).
+cell-updates/s (GCUPS) and % of the roofline at 1/2/4/8 GPUs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload weak|bit64k|byte16k]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload weak|strong262k|bit64k|byte16k]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workloads (a "step" = one pass of the hot path = one k-turn launch over the board):
-  weak     (default) bit-packed torus of 2^17 rows x 2^20 columns PER GPU, rows sharded
-           over the ranks with a k-row RCCL halo exchange (SURVEY.md §8(d) weak-scaling
-           config; N = 8 is the 2^20 x 2^20 torus of BASELINE.json config 5).
-  strong262k  262144 x 262144 bit-packed torus, rows sharded over the N ranks (config 4:
-           total work fixed as N grows, "scaling": "strong").
-  bit64k   65536 x 65536 bit-packed torus on one GPU (config 3); replicas for N > 1.
-  byte16k  16384 x 16384 byte-per-cell torus, 1 turn per step (config 2); replicas for N > 1.
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts its N ranks itself
+(child processes, before anything touches a GPU) and prints rank 0's line.
 
-Inputs are synthetic (splitmix64 Bernoulli(1/2) cells, generated on the GPU) and
-resident in HBM before timing.  Rank 0 prints one JSON line.
+Workloads (a "step" = one pass of the hot path = one k-turn launch over the whole board, with
+its halo exchange and the fused AliveCellsCount):
+  weak     (default) bit-packed torus of 2^17 rows x 2^20 columns PER GPU, rows sharded over the
+           ranks (one process per GPU, libgolhip's rank engine: RCCL halo exchange of k rows per
+           launch over xGMI, overlapped with the interior rows).  SURVEY.md §8(d)'s weak-scaling
+           config; N = 8 is BASELINE.json config 5's 2^20 x 2^20 torus.
+  strong262k  262144 x 262144 bit-packed torus sharded over the N ranks (config 4; total work
+           fixed as N grows, "scaling": "strong").
+  bit64k   65536 x 65536 bit-packed torus on one GPU (config 3); replicas for N > 1.
+  byte16k  16384 x 16384 byte-per-cell torus, k = 32 turns per launch (config 2); replicas for N > 1.
+
+Inputs are synthetic (splitmix64 Bernoulli(1/2) cells, generated on the GPU) and resident in
+HBM before timing.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,15 +37,15 @@ for _p in (ROOT, os.path.join(ROOT, "gol-distributed-final_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "cell-updates/sec (GCUPS) + % HBM roofline at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4  # wave64 VALU instructions/s: 1024 SIMDs x 1 per 2 cycles x 2.4 GHz
 BITS_BYTES_PER_UPDATE = 0.25  # 1 bit read + 1 bit written per cell per turn
 BYTES_BYTES_PER_UPDATE = 2.0  # 1 byte read + 1 byte written
+KERNEL_SRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernels.hip")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -46,206 +54,274 @@ def parse():
     ap.add_argument("--k", type=int, default=0,
                     help="turns per launch (temporal blocking); 0 = library default for bit boards "
                          "(12 band / 8 standard), 32 for byte16k")
-    ap.add_argument("--cpl", type=int, default=0, help="cells per lane (32/64/128; 0 = library default)")
-    ap.add_argument("--strip", type=int, default=0, help="rows per wave strip (0 = auto)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"],
-                    help="bit layout while stepping (auto = band when W %% 1024 == 0; DESIGN.md §4.1)")
+    ap.add_argument("--strip", type=int, default=0, help="rows per strip (0 = auto)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"])
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample length")
-    ap.add_argument("--no-count", action="store_true",
-                    help="do not fuse the alive-cell count (AliveCellsCount) into every launch")
-    ap.add_argument("--snapshot-rows", type=int, default=0,
-                    help="after the timed steps, stream this many board rows per rank as P5 bytes "
-                         "(device unpack -> host, golhip.sharded.stream_pgm's path) and report the rate "
-                         "(config 5's PGM snapshot; not part of value)")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--snapshot", default="",
+                    help="after the timed steps write the board as a P5 file here (every rank its own "
+                         "rows, gol_engine_write_pgm: config 5's snapshot); reported, not part of value")
     ap.add_argument("--share-gpu", action="store_true",
-                    help="testing only: every rank uses cuda:0 (multi-rank logic on a 1-GPU box, with --backend gloo)")
-    return ap.parse_args()
+                    help="testing only: every rank uses cuda:0 and runs an independent replica of its "
+                         "rows (RCCL refuses two ranks on one GPU); exercises the launcher, barriers "
+                         "and max-over-ranks timing on a 1-GPU box")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="orchestration only (no GPU): ranks, barriers and the JSON line, value 0")
+    return ap.parse_args(argv)
 
 
-def setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.share_gpu:
-        local = 0
-    torch.cuda.set_device(local)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
-    return rank, world, local
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def max_over_ranks(x: float, world: int) -> float:
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def self_launch(args) -> int:
+    """Start the N ranks as child processes (this process never touches the GPU) and print
+    rank 0's JSON line; nonzero exit if any rank fails."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0].decode(errors="replace")
+    rc = 0
+    for p in procs:
+        rc = rc or p.wait()
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return rc
 
 
-def barrier(world):
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+# ------------------------------------------------------------------ ranks
+class Ranks:
+    """torch.distributed (gloo, host side) for the barrier, max-over-ranks timing and sharing the
+    RCCL unique id; the board's own halo exchange and reductions are RCCL inside libgolhip."""
+
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={self.world}")
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            assert dist.get_world_size() == args.gpus
+            self.dist = dist
+        self.dry = args.dry_run
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        if not self.dry:
+            import torch
+            torch.cuda.synchronize()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t)
+        return float(t.item())
+
+    def share(self, obj):
+        if self.dist is None:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
 
 
-class KernelTimer:
-    """HIP events around every launch of one kind, on the stream the kernel runs on."""
-
-    def __init__(self, kinds):
-        self.kinds = set(kinds)
-        self.pairs = []
-        self.enabled = False
-        self._open = None
-
-    def __call__(self, kind, k, rows, before):
-        if not self.enabled or kind not in self.kinds:
-            return
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record(torch.cuda.current_stream())
-        if before:
-            self._open = (ev, k, rows)
-        else:
-            s, kk, rr = self._open
-            self.pairs.append((s, ev, kk, rr))
-
-    def avg(self):
-        ms = [s.elapsed_time(e) for s, e, _, _ in self.pairs]
-        return sum(ms) / len(ms), self.pairs[0][2], self.pairs[0][3]
-
-
-def cpu_baseline(args, H, W, k):
-    """Oracle restatement of the reference (literal worker.go port, one pthread per slab as the
-    broker's workers) on the host cores; bounded sample of the same synthetic board."""
-    from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    side = 1024
-    words = O.random_words(1, 0, side, side // 64)
-    board = O.unpack(words)
-    t0 = time.perf_counter()
-    O.run(board, 1, threads)
-    one = max(time.perf_counter() - t0, 1e-4)
-    turns = max(1, int(args.cpu_seconds / one))
-    t0 = time.perf_counter()
-    O.run(board, turns, threads)
-    dt = time.perf_counter() - t0
-    return {"value": side * side * turns / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": f"{side}x{side} torus (same splitmix64 board generator), {turns} turns, literal per-cell "
-                      f"port of worker.go:15-70 with the broker's {threads}-slab split (oracle/gol_oracle.c); "
-                      f"the Go reference cannot be built here"}
+# ------------------------------------------------------------------ measurement helpers
+def kernel_source_hash() -> str:
+    with open(KERNEL_SRC, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def load_pmc(key):
-    """Measured HBM bytes per launch for this exact configuration (tools/pmc_summary.py)."""
+    """PMC counters per launch of this workload's step kernel (tools/pmc_summary.py), only if they
+    were measured on the current gol_kernels.hip (sha256 prefix): a stale profile is not used."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(key)
+            e = json.load(f).get(key)
     except (OSError, ValueError):
-        return None
+        return None, "missing"
+    if not e:
+        return None, "missing"
+    if e.get("kernel_src") != kernel_source_hash():
+        return None, "stale (profiled on another gol_kernels.hip)"
+    return e, e.get("profile")
 
 
-def run_bits(args, rank, world):
-    from golhip.sharded import ShardedBoard
+def roofline(kind, launch_ms, cell_updates, pmc, pmc_note):
+    """The dominant kernel against its binding roof.  With k turns per launch the bit-board step
+    is bound by VALU issue: frac = wave64 VALU instructions per launch (PMC
+    SQ_INSTS_VALU) / (1024 SIMDs x 0.5 per cycle x 2.4 GHz x the live launch time).  The HBM side
+    (PMC bytes per launch / live time vs 8 TB/s) and the SURVEY §8(d) effective-bandwidth figure
+    (algorithmic bytes / time) are reported beside it under their own keys."""
+    bpu = BITS_BYTES_PER_UPDATE if kind == "bits" else BYTES_BYTES_PER_UPDATE
+    sec = launch_ms * 1e-3
+    eff = bpu * cell_updates / sec / 1e9
+    traffic = pmc.get("bytes_per_launch") if pmc else None
+    hbm = {"achieved": round(traffic / sec / 1e9, 1) if traffic else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4) if traffic else None}
+    r = {"launch_ms": round(launch_ms, 4), "cell_updates_per_launch": cell_updates,
+         "effective_GBs": round(eff, 1),
+         "effective_basis": f"{bpu} B/cell-update (SURVEY.md §8(d)) x {cell_updates:.4g} cell-updates per launch "
+                            f"/ {launch_ms:.3f} ms mean launch (HIP events on the launch stream)",
+         "traffic": traffic, "hbm": hbm, "pmc": pmc_note}
+    valu = pmc.get("valu_insts_per_launch") if pmc else None
+    if valu:
+        ach = valu / sec / 1e9
+        r.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
+                  "unit": "G wave64 VALU inst/s", "frac": round(ach / VALU_PEAK_GINST, 4)})
+    else:  # no PMC profile of this kernel build: only the HBM side can be stated (None without traffic)
+        r.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": hbm["frac"]})
+    return r
+
+
+def cpu_baseline(args):
+    """The oracle's literal port of worker.go:15-70 with the broker's slab split (one pthread per
+    slab, broker.go:135-206) on config 1: images/512x512.pgm, 100 turns, 4 slabs (the reference's
+    broker + 4 workers), plus 1 thread and every allowed core.  The Go reference cannot be built
+    (no Go toolchain here or on the GPU box)."""
+    import numpy as np
+    from oracle import oracle as O
+    golden = os.path.join(ROOT, "tests", "golden")
+    _, _, board = O.read_pgm(os.path.join(golden, "images", "512x512.pgm"), 512, 512)
+    want = O.read_pgm(os.path.join(golden, "check", "images", "512x512x100.pgm"))[2]
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    allowed = min(allowed, 16)  # the GPU box's CPU share (16 cores per GPU); os.cpu_count() is the whole host
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    res = {}
+    for threads in sorted({1, 4, allowed}):
+        times = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            out = O.run(board, 100, threads)
+            times.append(time.perf_counter() - t0)
+        assert np.array_equal(out, want), "cpu baseline disagrees with check/images/512x512x100.pgm"
+        times.sort()
+        res[threads] = 512 * 512 * 100 / times[2] / 1e9
+    return {"value": round(res[4], 4), "unit": "GCUPS", "cores": 4, "kind": "port",
+            "sample": "config 1: images/512x512.pgm, 100 turns, 4 slabs (one pthread per slab = the broker's 4 "
+                      "workers), median of 5, result checked against check/images/512x512x100.pgm; literal "
+                      "per-cell port of worker.go:15-70 (oracle/gol_oracle.c), the Go reference cannot be built",
+            "GCUPS_1_thread": round(res[1], 4), f"GCUPS_{allowed}_threads": round(res[allowed], 4),
+            "cpu_count": os.cpu_count(), "cpu_share": allowed, "cpu_model": model}
+
+
+# ------------------------------------------------------------------ workloads
+def run_bits(args, ranks):
+    import golhip
+    world, rank = ranks.world, ranks.rank
     if args.workload == "weak":
-        H, W, nshards = args.rows_per_gpu * world, args.width, world
+        H, W, sharded = args.rows_per_gpu * world, args.width, True
     elif args.workload == "strong262k":
-        H, W, nshards = 262144, 262144, world
+        H, W, sharded = 262144, 262144, True
     else:
-        H, W, nshards = 65536, 65536, 1
-    group = None
-    if nshards == 1 and world > 1:  # independent replicas: every rank its own board, no collective
-        group = [dist.new_group([r]) for r in range(world)][rank]
-    board = ShardedBoard(H, W, turns_per_launch=args.k, cells_per_lane=args.cpl, strip_rows=args.strip,
-                         group=group, layout=args.layout)
-    layout = "band" if board.use_band else "standard"
-    k = board.kmax
-    board.load_random(1)
-    timer = KernelTimer(["full", "interior"])
-    board.launch_hook = timer
-    count = not args.no_count  # AliveCellsCount fused into the last generation of every launch
-    for _ in range(args.warmup):
-        board.step(k, count=count)
-    barrier(world)
-    timer.enabled = True
+        H, W, sharded = 65536, 65536, False
+    if args.share_gpu and sharded and world > 1:
+        # test mode: every rank an independent 1-GPU replica of rows_per_gpu rows
+        H, sharded = H // world, False
+    kw = dict(device=ranks.local, turns_per_launch=args.k, strip_rows=args.strip, layout=args.layout)
+    if sharded and world > 1:
+        uid = ranks.share(golhip.engine.rccl_unique_id() if rank == 0 else None)
+        e = golhip.Engine.rank(H, W, world, rank, uid, **kw)
+        topo = e.topology()
+        assert topo["nranks"] == world and topo["transport"] == "rccl", topo
+    else:
+        e = golhip.Engine(H, W, **kw)
+        topo = e.topology()
+    info = e.info()
+    k = info["turns_per_launch"]
+    e.load_random(1)
+    if args.warmup:
+        e.step_counted(args.warmup * k, k)
+    ranks.barrier()
+    e.set_timing(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        board.step(k, count=count)
-    torch.cuda.synchronize()
+    counts = e.step_counted(args.steps * k, k)  # one launch (+ halo exchange + fused count) per step
     dt = time.perf_counter() - t0
-    barrier(world)
-    timer.enabled = False
-    dt = max_over_ranks(dt, world)
-    alive = board.fused_count() if count else None
-    cells_total = H * W * (world if nshards == 1 else 1)
+    ranks.barrier()
+    t = e.timing()
+    e.set_timing(False)
+    dt = ranks.max(dt)
+    alive = int(counts[-1]) if len(counts) else None
+    if not sharded and world > 1:
+        cells_total = ranks.sum(H * W)  # independent replicas
+        alive = int(ranks.sum(alive))
+    else:
+        cells_total = H * W
     value = cells_total * k * args.steps / dt
-    kms, kk, krows = timer.avg()
-    alg_bytes = BITS_BYTES_PER_UPDATE * krows * W * kk
-    achieved = alg_bytes / (kms * 1e-3) / 1e9
-    from golhip import lib
-    info = {"turns_per_step": k, "layout": layout,
-            "cells_per_lane": 128 if layout == "band" else (args.cpl or "lib default (64)"),
-            "strip_rows": args.strip or "auto",
-            "alive_count_every_step": count, "alive_final": alive, "turns_done": board.turn}
-    pmc = load_pmc(f"{args.workload}:{H}x{W}:n{world}:k{k}:" + ("band" if layout == "band" else f"cpl{args.cpl}"))
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc.get("bytes_per_launch") if pmc else None,
-            # with k turns per launch the kernel is bound by VALU issue, not HBM (DESIGN.md §4.1):
-            # the PMC-measured share of the 2-cycle VALU issue peak, from the same profile
-            "valu_issue_frac": pmc.get("valu_issue_frac") if pmc else None,
-            "basis": f"{BITS_BYTES_PER_UPDATE} B/cell-update x {krows}x{W} cells x {kk} turns per launch "
-                     f"/ {kms:.3f} ms mean launch ({len(timer.pairs)} launches, HIP events)",
-            "hbm_min_bytes_frac": round(2 * krows * W / 8 / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    del lib
+    snap = None
+    if args.snapshot:
+        ranks.barrier()
+        s0 = time.perf_counter()
+        e.write_pgm(args.snapshot)
+        sdt = ranks.max(time.perf_counter() - s0)
+        snap = {"path": args.snapshot, "bytes": H * W, "GB_per_s": round(H * W / sdt / 1e9, 3),
+                "note": "device unpack + D2H + pwrite of every rank's rows (PCIe and disk inclusive)"}
+    layout = {0: "bytes", 1: "standard", 2: "band"}[2 if info["layout"] == "band" else 1]
+    key = f"{args.workload}:{args.rows_per_gpu if args.workload == 'weak' else H}x{W}:k{k}:{layout}"
+    pmc, note = load_pmc(key)
+    roof = roofline("bits", t["mean_ms"], t["mean_cell_updates"], pmc, note)
     rpg = args.rows_per_gpu
     rows_name = f"2^{rpg.bit_length() - 1}" if rpg & (rpg - 1) == 0 else str(rpg)
     wname = f"2^{W.bit_length() - 1}" if W & (W - 1) == 0 else str(W)
-    snap = snapshot(board, args.snapshot_rows, world) if args.snapshot_rows > 0 else None
     name = {"weak": f"weak-{rows_name}x{wname}-per-gpu", "strong262k": "strong-262144x262144",
             "bit64k": "bit-65536x65536"}[args.workload]
-    cfg = {"workload": name,
-           "H": H, "W": W, "parallelism": (f"rows{world}" if nshards > 1 else (f"replicas{world}" if world > 1 else "1gpu")),
-           **info}
-    if snap is not None:
+    cfg = {"workload": name, "H": H, "W": W, "parallelism": (f"rows{world}" if sharded and world > 1 else
+                                   (f"replicas{world}" if world > 1 else "1gpu")),
+           "transport": topo["transport"], "turns_per_step": k, "layout": layout,
+           "cells_per_lane": info["cells_per_lane"], "strip_rows": args.strip or "auto",
+           "alive_count_every_step": True, "alive_final": alive, "turns_done": (args.warmup + args.steps) * k,
+           "timed_launches": t["launches"]}
+    if snap:
         cfg["snapshot"] = snap
+    e.close()
     dtype = "u32 (bit-packed, 32 cells/word" + (", column-band layout)" if layout == "band" else ")")
     return value, dt, cfg, roof, dtype
 
 
-def snapshot(board, rows, world):
-    """Config 5's PGM snapshot path, bounded: every rank unpacks its first `rows` rows on the GPU
-    (bits -> 0/255 bytes, golhip.sharded.stream_pgm's chunked path) and copies them to the host;
-    reported as host bytes/s over all ranks (PCIe-inclusive, not part of value)."""
-    rows = min(rows, board.R)
-    std = board.standard()
-    chunk = 4096
-    barrier(world)
-    t0 = time.perf_counter()
-    n = 0
-    for a in range(0, rows, chunk):
-        part = board.kern.unpack(std[a:a + min(chunk, rows - a)], board.W)
-        n += part.cpu().numpy().nbytes
-    torch.cuda.synchronize()
-    dt = max_over_ranks(time.perf_counter() - t0, world)
-    return {"rows_per_rank": rows, "bytes": n * world, "GB_per_s": round(n * world / dt / 1e9, 2)}
+def run_bytes(args, ranks):
+    """Config 2: 16384 x 16384 byte-per-cell torus.  The board stays one byte per cell in HBM; each
+    launch runs k turns (gol_dev_bytes_step_k: 0/255 bytes packed to bits in registers); k = 1
+    is the exact one-turn byte kernel (gol_dev_bytes_step)."""
+    import ctypes
 
-
-def run_bytes(args, rank, world):
-    """Config 2: 16384 x 16384 byte-per-cell torus.  The board stays one byte per cell in HBM;
-    with --k > 1 each launch runs k turns (gol_dev_bytes_step_k: 0/255 bytes packed to bits in
-    registers), with --k 1 the exact one-turn byte kernel (gol_dev_bytes_step)."""
+    import torch
     from golhip._lib import check, lib
     from golhip.sharded import HipKernels
+    torch.cuda.set_device(ranks.local)
     H = W = 16384
     Wd = W // 32
     bits = torch.empty((H, Wd), dtype=torch.int32, device="cuda")
@@ -255,6 +331,7 @@ def run_bytes(args, rank, world):
     a = kern.unpack(bits, W)
     b = torch.empty_like(a)
     del bits
+    slots = torch.zeros(256 * 8, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     k = max(kk for kk in (32, 16, 8, 4, 2, 1) if kk <= args.k)
     pairs = []
@@ -268,8 +345,9 @@ def run_bytes(args, rank, world):
         if k == 1:
             check(lib().gol_dev_bytes_step(src.data_ptr(), H, W, W, 0, H, dst.data_ptr(), W, stream))
         else:
+            slots.zero_()
             check(lib().gol_dev_bytes_step_k(src[H - k:].data_ptr(), src.data_ptr(), src.data_ptr(), dst.data_ptr(),
-                                             H, W, W, 0, H, k, args.strip, None, stream))
+                                             H, W, W, 0, H, k, args.strip, slots.data_ptr(), stream))
         if timed:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
@@ -278,51 +356,54 @@ def run_bytes(args, rank, world):
 
     for _ in range(args.warmup):
         step(False)
-    barrier(world)
+    ranks.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    barrier(world)
-    dt = max_over_ranks(dt, world)
-    value = H * W * world * k * args.steps / dt
+    ranks.barrier()
+    flags = ctypes.c_uint32()
+    check(lib().gol_dev_error(ranks.local, ctypes.byref(flags)))
+    dt = ranks.max(dt)
+    value = H * W * ranks.world * k * args.steps / dt
     kms = sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
-    achieved = BYTES_BYTES_PER_UPDATE * H * W * k / (kms * 1e-3) / 1e9
-    pmc = load_pmc(f"byte16k:{H}x{W}:n1:k{k}:cpl0")
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("bytes_per_launch") if pmc else None,
-            "basis": f"{BYTES_BYTES_PER_UPDATE} B/cell-update x {H}x{W} cells x {k} turns per launch / "
-                     f"{kms:.3f} ms mean launch",
-            "hbm_min_bytes_frac": round(2 * H * W / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    alive = int(slots.view(256, 8)[:, 0].sum().item()) if k > 1 else None
+    pmc, note = load_pmc(f"byte16k:{H}x{W}:k{k}:bytes")
+    roof = roofline("bytes", kms, float(H * W * k), pmc, note)
     cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k,
-           "parallelism": f"replicas{world}" if world > 1 else "1gpu"}
+           "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "1gpu",
+           "alive_count_every_step": k > 1, "alive_final": alive, "turns_done": (args.warmup + args.steps) * k}
     return value, dt, cfg, roof, "u8 (byte per cell)"
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     if args.k <= 0 and args.workload == "byte16k":
-        args.k = 32  # pipelined byte kernel, 8 waves x 4 turns; bit boards: 0 = library default (12 on the band layout, 8 on the standard one)
-    rank, world, local = setup(args)
-    if args.workload == "byte16k":
-        value, dt, cfg, roof, dtype = run_bytes(args, rank, world)
+        args.k = 32  # pipelined byte kernel, 8 waves x 4 turns
+    ranks = Ranks(args)
+    if args.dry_run:
+        ranks.barrier()
+        dt = ranks.max(0.001 * (ranks.rank + 1))
+        value, cfg, roof, dtype = 0.0, {"workload": "dry-run", "ranks": ranks.world}, None, None
+    elif args.workload == "byte16k":
+        value, dt, cfg, roof, dtype = run_bytes(args, ranks)
     else:
-        value, dt, cfg, roof, dtype = run_bits(args, rank, world)
+        value, dt, cfg, roof, dtype = run_bits(args, ranks)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, cfg["H"], cfg["W"], cfg.get("turns_per_step", 1))
-    if rank == 0:
-        line = {"metric": "cell-updates/sec (GCUPS) + % HBM roofline at 1/2/4/8 MI355X", "value": round(value / 1e9, 2),
-                "unit": "GCUPS", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-                "scaling": "strong" if args.workload == "strong262k" else "weak", "vs_baseline": None,
-                "dtype": dtype,
+    if ranks.rank == 0 and ranks.world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        cpu = cpu_baseline(args)
+    if ranks.rank == 0:
+        line = {"metric": METRIC, "value": round(value / 1e9, 2), "unit": "GCUPS", "n_gpus": ranks.world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "higher_is_better": True, "scaling": "strong" if args.workload == "strong262k" else "weak",
+                "vs_baseline": None, "dtype": dtype,
                 "data": "synthetic (splitmix64 Bernoulli(1/2) torus generated on the GPU)",
                 "config": cfg, "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ranks.close()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,1191 @@
+// gol_engine.cpp -- the board engine of libgolhip.so: a Game-of-Life torus resident in HBM,
+// on one GPU or row-sharded over several (include/golhip.h, "engine").
+//
+// The reference keeps the board in the broker and ships ALL of it to every worker every turn
+// (broker.go:143-157, 182-211), then gathers the slabs and copies them into cWorld
+// (broker.go:153-169).  Here the broker's row partition (broker.go:135-206) is applied once,
+// to GPUs: shard r keeps rows [y0_r, y1_r) bit-packed in its own HBM for the whole run, and the
+// only traffic between shards is a k-row halo every k turns (RCCL send/recv over xGMI, or
+// device copies between the shards of one process).
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "golhip.h"
+#include "gol_internal.h"
+#include "gol_kernels.h"
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return gol_set_error(e_ == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP, "%s failed: %s (%s:%d)", #expr, \
+                                 hipGetErrorString(e_), __FILE__, __LINE__);                      \
+    } while (0)
+
+#define NCCLCHK(expr)                                                                             \
+    do {                                                                                          \
+        ncclResult_t r_ = (expr);                                                                 \
+        if (r_ != ncclSuccess)                                                                    \
+            return gol_set_error(GOL_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(r_));      \
+    } while (0)
+
+#define RCCHK(expr)                  \
+    do {                             \
+        int rc_ = (expr);            \
+        if (rc_ != GOL_OK) return rc_; \
+    } while (0)
+
+static constexpr size_t SLOT_BYTES = GOL_COUNT_SLOTS * 8 * sizeof(uint64_t);
+
+static int set_dev(int d)
+{
+    HIPCHK(hipSetDevice(d));
+    return GOL_OK;
+}
+
+// Turns per launch: the largest supported k <= want, the remaining turns and the smallest
+// shard.  k = 12 is the band layout's split pipeline (4 words per lane); k = 16 needs <= 2
+// words per lane.
+static int pick_k(int want, int64_t remaining, int64_t rows, int dw, bool band)
+{
+    static const int ks[] = {16, 12, 8, 4, 2, 1};
+    for (int k : ks) {
+        if (k == 16 && dw > 2) continue;
+        if (k == 12 && !(band && dw == 4)) continue;
+        if (k <= want && k <= remaining && k <= rows) return k;
+    }
+    return 1;
+}
+
+// ------------------------------------------------------------------ allocation
+static int ensure_staging(gol_engine *e, gol_shard &s)
+{
+    if (!s.staging) {
+        // byte staging for chunked load/store/PGM: >= 1 row, <= 64 MiB
+        const int64_t rows = std::max<int64_t>(s.R, 1);
+        s.stage_rows = std::max<int64_t>(1, std::min<int64_t>(rows, (64LL << 20) / e->bstride));
+        HIPCHK(hipMalloc(&s.staging, s.stage_rows * e->bstride));
+        HIPCHK(hipHostMalloc((void **)&s.host_staging, s.stage_rows * e->bstride, hipHostMallocDefault));
+    }
+    return GOL_OK;
+}
+
+static int ensure_counts(gol_shard &s, int64_t n)
+{
+    if (s.counts_cap >= n) return GOL_OK;
+    if (s.counts) (void)hipFree(s.counts);
+    s.counts = nullptr;
+    s.counts_cap = 0;
+    const int64_t cap = std::max<int64_t>(n, 64);
+    HIPCHK(hipMalloc(&s.counts, cap * sizeof(uint64_t)));
+    s.counts_cap = cap;
+    return GOL_OK;
+}
+
+static void free_exact_bytes(gol_shard &s)
+{
+    for (auto &b : s.bytes)
+        if (b) { (void)hipFree(b); b = nullptr; }
+}
+
+static void shard_release(gol_shard &s)
+{
+    (void)hipSetDevice(s.device);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.comm) (void)hipStreamSynchronize(s.comm);
+    if (s.nccl) (void)ncclCommDestroy(s.nccl);
+    for (auto &b : s.bits_alloc)
+        if (b) (void)hipFree(b);
+    free_exact_bytes(s);
+    if (s.slots) (void)hipFree(s.slots);
+    if (s.counts) (void)hipFree(s.counts);
+    if (s.flag) (void)hipFree(s.flag);
+    if (s.err) (void)hipFree(s.err);
+    if (s.host_word) (void)hipHostFree(s.host_word);
+    if (s.staging) (void)hipFree(s.staging);
+    if (s.host_staging) (void)hipHostFree(s.host_staging);
+    for (auto ev : s.tev) (void)hipEventDestroy(ev);
+    if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
+    if (s.ev_comm) (void)hipEventDestroy(s.ev_comm);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.comm) (void)hipStreamDestroy(s.comm);
+    s = gol_shard();
+}
+
+static int shard_alloc(gol_engine *e, gol_shard &s)
+{
+    RCCHK(set_dev(s.device));
+    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_comm, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&s.slots, SLOT_BYTES));
+    HIPCHK(hipMalloc(&s.flag, sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&s.err, sizeof(uint32_t)));
+    HIPCHK(hipHostMalloc((void **)&s.host_word, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    // on the shard's stream: it is non-blocking, so a null-stream memset could still be running
+    // when the first load or fill kernel writes the board
+    HIPCHK(hipMemsetAsync(s.err, 0, sizeof(uint32_t), s.stream));
+    if (e->bit_capable) {
+        const int64_t rows = s.R + 2 * GOL_GHOST_ROWS;
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(hipMalloc(&s.bits_alloc[i], rows * e->pitch * sizeof(uint32_t)));
+            HIPCHK(hipMemsetAsync(s.bits_alloc[i], 0, rows * e->pitch * sizeof(uint32_t), s.stream));
+            s.bits[i] = s.bits_alloc[i] + GOL_GHOST_ROWS * e->pitch;
+        }
+    } else {
+        for (auto &b : s.bytes) HIPCHK(hipMalloc(&b, e->H * e->bstride));
+        HIPCHK(hipMemsetAsync(s.bytes[0], 0, e->H * e->bstride, s.stream));
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return GOL_OK;
+}
+
+// Board geometry and kernel parameters from the configuration (shared by both constructors).
+static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *cfg)
+{
+    if (H <= 0 || W <= 0 || W > (int64_t)INT32_MAX * 32 || H > INT32_MAX)
+        return gol_set_error(GOL_EINVAL, "bad board size %lldx%lld", (long long)W, (long long)H);
+    e->H = H;
+    e->W = W;
+    e->bit_capable = (W % 64) == 0;
+    e->mode = e->bit_capable ? GOL_MODE_BITS : GOL_MODE_BYTES;
+    e->Wd = W / 32;
+    e->pitch = (e->Wd + 3) / 4 * 4;
+    e->bstride = (W + 15) / 16 * 16;
+    e->k = (cfg && cfg->turns_per_launch > 0) ? cfg->turns_per_launch : 0;  // 0: per layout, below
+    const int req = cfg ? cfg->cells_per_lane : 0;
+    const int cpl = req > 0 ? req : 32 * GOL_DEFAULT_DW;
+    if (cpl != 32 && cpl != 64 && cpl != 128) return gol_set_error(GOL_EINVAL, "cells_per_lane must be 32, 64 or 128");
+    e->dw = cpl / 32;
+    while (e->dw > 1 && (e->Wd % e->dw) != 0) e->dw >>= 1;
+    e->band_dw = req == 64 ? 2 : (req == 128 ? 4 : GOL_BAND_DEFAULT_DW);
+    e->strip = cfg ? cfg->strip_rows : 0;
+    const int layout = cfg ? cfg->layout : GOL_LAYOUT_AUTO;
+    if (layout != GOL_LAYOUT_AUTO && layout != GOL_LAYOUT_STANDARD && layout != GOL_LAYOUT_BAND)
+        return gol_set_error(GOL_EINVAL, "layout must be GOL_LAYOUT_AUTO, _STANDARD or _BAND");
+    if (layout == GOL_LAYOUT_BAND && W % 1024 != 0) return gol_set_error(GOL_EINVAL, "the band layout needs W %% 1024 == 0");
+    e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
+    if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
+    return GOL_OK;
+}
+
+// Shards [0, n) of this process are global ranks e->rank + i of e->nranks.
+static int engine_shards(gol_engine *e, const std::vector<int> &devices)
+{
+    if (e->nranks > 1 && !e->bit_capable)
+        return gol_set_error(GOL_EINVAL, "a sharded board needs W %% 64 == 0 (W = %lld)", (long long)e->W);
+    if (e->H < e->nranks)
+        return gol_set_error(GOL_EINVAL, "%d shards cannot split %lld rows", e->nranks, (long long)e->H);
+    e->min_rows = e->H / e->nranks;  // broker.go:172-206: the smallest shard
+    e->sh.resize(devices.size());
+    for (size_t i = 0; i < devices.size(); ++i) {
+        gol_shard &s = e->sh[i];
+        s.device = devices[i];
+        const int64_t r = e->rank + (int64_t)i;
+        int rc = gol_partition_rows(e->H, e->nranks, r, &s.y0, &s.y1);
+        if (rc) return rc;
+        s.R = s.y1 - s.y0;
+        RCCHK(shard_alloc(e, s));
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, gol_engine **out)
+{
+    if (!out) return gol_set_error(GOL_EINVAL, "out is NULL");
+    *out = nullptr;
+    gol_engine *e = new gol_engine();
+    int rc = engine_setup(e, H, W, cfg);
+    const int n = cfg && cfg->shards > 1 ? cfg->shards : 1;
+    const int same = cfg && (cfg->flags & GOL_SHARDS_SAME_DEVICE);
+    int transport = cfg ? cfg->transport : GOL_TRANSPORT_AUTO;
+    std::vector<int> devs(n);
+    if (rc == GOL_OK) {
+        int dev0 = cfg ? cfg->device : -1, ndev = 0;
+        if (dev0 < 0 && hipGetDevice(&dev0) != hipSuccess) dev0 = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            rc = gol_set_error(GOL_EHIP, "no HIP device");
+        for (int i = 0; rc == GOL_OK && i < n; ++i) devs[i] = same ? dev0 : (dev0 + i) % ndev;
+        std::vector<int> sorted(devs);
+        std::sort(sorted.begin(), sorted.end());
+        const bool distinct = std::unique(sorted.begin(), sorted.end()) == sorted.end();
+        if (transport == GOL_TRANSPORT_AUTO)
+            transport = n == 1 ? GOL_TRANSPORT_LOCAL : (distinct ? GOL_TRANSPORT_RCCL : GOL_TRANSPORT_LOOPBACK);
+        if (transport != GOL_TRANSPORT_LOCAL && transport != GOL_TRANSPORT_LOOPBACK && transport != GOL_TRANSPORT_RCCL)
+            rc = gol_set_error(GOL_EINVAL, "unknown transport %d", transport);
+        if (transport == GOL_TRANSPORT_LOCAL && n > 1) rc = gol_set_error(GOL_EINVAL, "the local transport has one shard");
+    }
+    e->nranks = n;
+    e->rank = 0;
+    e->transport = transport;
+    if (rc == GOL_OK) rc = engine_shards(e, devs);
+    if (rc == GOL_OK && transport == GOL_TRANSPORT_RCCL) {
+        std::vector<ncclComm_t> comms(n);
+        ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+        if (r != ncclSuccess) rc = gol_set_error(GOL_ECOMM, "ncclCommInitAll(%d GPUs): %s", n, ncclGetErrorString(r));
+        else
+            for (int i = 0; i < n; ++i) e->sh[i].nccl = comms[i];
+    }
+    if (rc == GOL_OK && transport == GOL_TRANSPORT_LOOPBACK)  // peer access between distinct GPUs (copies work without)
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j)
+                if (devs[i] != devs[j] && hipSetDevice(devs[i]) == hipSuccess) {
+                    (void)hipDeviceEnablePeerAccess(devs[j], 0);
+                    (void)hipGetLastError();
+                }
+    if (rc != GOL_OK) {
+        gol_engine_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+extern "C" int gol_rccl_unique_id(uint8_t *id, int64_t len)
+{
+    if (!id || len < (int64_t)sizeof(ncclUniqueId)) return gol_set_error(GOL_EINVAL, "id needs %d bytes", GOL_RCCL_ID_BYTES);
+    ncclUniqueId u;
+    NCCLCHK(ncclGetUniqueId(&u));
+    memcpy(id, &u, sizeof u);
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int32_t rank, const uint8_t *id,
+                                      const gol_config *cfg, gol_engine **out)
+{
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || (!id && nranks > 1))
+        return gol_set_error(GOL_EINVAL, "bad rank arguments (rank %d of %d)", rank, nranks);
+    if (cfg && cfg->shards > 1) return gol_set_error(GOL_EINVAL, "one shard per rank");
+    *out = nullptr;
+    gol_engine *e = new gol_engine();
+    int rc = engine_setup(e, H, W, cfg);
+    int dev = cfg ? cfg->device : -1;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    int transport = cfg ? cfg->transport : GOL_TRANSPORT_AUTO;
+    if (transport == GOL_TRANSPORT_AUTO) transport = nranks > 1 ? GOL_TRANSPORT_RCCL : GOL_TRANSPORT_LOCAL;
+    if (rc == GOL_OK && transport != GOL_TRANSPORT_RCCL && !(transport == GOL_TRANSPORT_LOCAL && nranks == 1))
+        rc = gol_set_error(GOL_EINVAL, "ranks in several processes exchange halos over RCCL");
+    e->nranks = nranks;
+    e->rank = rank;
+    e->rank_mode = true;
+    e->transport = transport;
+    if (rc == GOL_OK) rc = engine_shards(e, {dev});
+    if (rc == GOL_OK && transport == GOL_TRANSPORT_RCCL) {
+        ncclUniqueId u;
+        if (id) memcpy(&u, id, sizeof u);
+        else if (ncclGetUniqueId(&u) != ncclSuccess) rc = gol_set_error(GOL_ECOMM, "ncclGetUniqueId failed");
+        ncclResult_t r = rc == GOL_OK ? ncclCommInitRank(&e->sh[0].nccl, nranks, u, rank) : ncclSuccess;
+        if (r != ncclSuccess) rc = gol_set_error(GOL_ECOMM, "ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(r));
+    }
+    if (rc != GOL_OK) {
+        gol_engine_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+extern "C" void gol_engine_destroy(gol_engine *e)
+{
+    if (!e) return;
+    for (auto &s : e->sh) shard_release(s);
+    delete e;
+}
+
+extern "C" int gol_engine_topology(gol_engine *e, int32_t *shards, int32_t *nranks, int32_t *rank, int32_t *transport)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    if (shards) *shards = (int32_t)e->sh.size();
+    if (nranks) *nranks = e->nranks;
+    if (rank) *rank = e->rank;
+    if (transport) *transport = e->transport;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_shard(gol_engine *e, int32_t i, int32_t *device, int64_t *y0, int64_t *y1)
+{
+    if (!e || i < 0 || i >= (int32_t)e->sh.size()) return gol_set_error(GOL_EINVAL, "no local shard %d", i);
+    if (device) *device = e->sh[i].device;
+    if (y0) *y0 = e->sh[i].y0;
+    if (y1) *y1 = e->sh[i].y1;
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------ synchronisation, errors
+// Wait for every shard's work and read the shards' device error words (one pinned readback
+// queued behind the work, so the check costs no extra synchronisation).
+static int sync_all(gol_engine *e)
+{
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemcpyAsync(s.host_word, s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+    }
+    uint32_t flags = 0;
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipStreamSynchronize(s.comm));
+        flags |= s.host_word[0];
+    }
+    if (flags) {
+        for (auto &s : e->sh) {
+            RCCHK(set_dev(s.device));
+            HIPCHK(hipMemset(s.err, 0, sizeof(uint32_t)));
+        }
+        return gol_set_error(GOL_EHIP, "device fault in a step kernel (error flags 0x%x: %s); the board is not valid",
+                             flags, (flags & GOLK_ERR_SPIN) ? "a pipeline wave timed out waiting for its neighbour" : "?");
+    }
+    if (e->mode == GOL_MODE_BITS)
+        for (auto &s : e->sh) free_exact_bytes(s);  // the exact first turn's byte rows, once used
+    return GOL_OK;
+}
+
+// Collective barrier of the ranks of a several-process engine (a one-element all-reduce).
+static int rank_barrier(gol_engine *e)
+{
+    if (!e->rank_mode || e->nranks == 1) return GOL_OK;
+    gol_shard &s = e->sh[0];
+    RCCHK(set_dev(s.device));
+    NCCLCHK(ncclAllReduce(s.flag, s.flag, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------ layout conversion
+// The band layout is a stepping detail: convert on the first step, convert back before
+// anything reads the bits.  Both are one HBM pass (32x32 bit transposes) per shard.
+static int convert(gol_engine *e, bool to_band)
+{
+    if (e->band == to_band || e->mode != GOL_MODE_BITS) return GOL_OK;
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(golk_band_convert(to_band, s.bits[e->cur], s.bits[1 - e->cur], s.R, e->Wd, e->pitch, e->pitch, s.stream));
+    }
+    e->cur = 1 - e->cur;
+    e->band = to_band;
+    return GOL_OK;
+}
+static int ensure_standard(gol_engine *e) { return convert(e, false); }
+
+// ------------------------------------------------------------------ one k-turn launch
+static int copy_rows(gol_shard &dst_s, uint32_t *dst, const gol_shard &src_s, const uint32_t *src, size_t bytes,
+                     hipStream_t st)
+{
+    if (dst_s.device == src_s.device) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+    else HIPCHK(hipMemcpyPeerAsync(dst, dst_s.device, src, src_s.device, bytes, st));
+    return GOL_OK;
+}
+
+// Halo rows of the current input buffer: shard r's ghost rows [-k, 0) <- the last k rows of
+// shard r-1, ghost rows [R, R+k) <- the first k rows of shard r+1 (mod nranks).
+static int exchange(gol_engine *e, int k)
+{
+    const int n = (int)e->sh.size();
+    const int c = e->cur;
+    const int64_t P = e->pitch;
+    const size_t hb = (size_t)k * P * sizeof(uint32_t);
+    if (e->transport == GOL_TRANSPORT_LOCAL) {  // one shard = the whole torus: wrap rows on its own stream
+        gol_shard &s = e->sh[0];
+        uint32_t *mid = s.bits[c];
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemcpyAsync(mid - k * P, mid + (s.R - k) * P, hb, hipMemcpyDeviceToDevice, s.stream));
+        HIPCHK(hipMemcpyAsync(mid + s.R * P, mid, hb, hipMemcpyDeviceToDevice, s.stream));
+        return GOL_OK;
+    }
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipEventRecord(s.ev_ready, s.stream));
+    }
+    if (e->transport == GOL_TRANSPORT_LOOPBACK) {
+        for (int i = 0; i < n; ++i) {
+            gol_shard &s = e->sh[i], &p = e->sh[(i + n - 1) % n], &q = e->sh[(i + 1) % n];
+            RCCHK(set_dev(s.device));
+            HIPCHK(hipStreamWaitEvent(s.comm, s.ev_ready, 0));  // my ghost rows are no longer read
+            HIPCHK(hipStreamWaitEvent(s.comm, p.ev_ready, 0));  // the neighbours' rows are written
+            HIPCHK(hipStreamWaitEvent(s.comm, q.ev_ready, 0));
+            RCCHK(copy_rows(s, s.bits[c] - k * P, p, p.bits[c] + (p.R - k) * P, hb, s.comm));
+            RCCHK(copy_rows(s, s.bits[c] + s.R * P, q, q.bits[c], hb, s.comm));
+            HIPCHK(hipEventRecord(s.ev_comm, s.comm));
+        }
+        return GOL_OK;
+    }
+    // RCCL: one group over every local shard (ncclCommInitAll comms must be driven together).
+    // For two ranks both neighbours are the same peer: the issue order pairs my first send
+    // (top rows) with the peer's first receive (its bottom ghost rows), as the ring requires.
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamWaitEvent(s.comm, s.ev_ready, 0));
+    }
+    const size_t cnt = (size_t)k * P;
+    ncclResult_t first = ncclGroupStart();
+    for (int i = 0; i < n && first == ncclSuccess; ++i) {
+        gol_shard &s = e->sh[i];
+        const int N = e->nranks, r = e->rank + i;
+        const int prev = (r + N - 1) % N, next = (r + 1) % N;
+        uint32_t *mid = s.bits[c];
+        ncclResult_t x;
+        if ((x = ncclSend(mid, cnt, ncclUint32, prev, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
+        if ((x = ncclRecv(mid + s.R * P, cnt, ncclUint32, next, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
+        if ((x = ncclSend(mid + (s.R - k) * P, cnt, ncclUint32, next, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
+        if ((x = ncclRecv(mid - k * P, cnt, ncclUint32, prev, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
+    }
+    const ncclResult_t end = ncclGroupEnd();
+    if (first != ncclSuccess || end != ncclSuccess)
+        return gol_set_error(GOL_ECOMM, "halo exchange: %s", ncclGetErrorString(first != ncclSuccess ? first : end));
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipEventRecord(s.ev_comm, s.comm));
+    }
+    return GOL_OK;
+}
+
+static int shard_kernel(gol_engine *e, int i, int k, int64_t row0, int64_t rows, uint64_t *slots, bool timed)
+{
+    gol_shard &s = e->sh[i];
+    if (rows <= 0) return GOL_OK;
+    uint32_t *mid = s.bits[e->cur];
+    const uint32_t *top = mid - (int64_t)k * e->pitch, *bot = mid + s.R * e->pitch;
+    uint32_t *dst = s.bits[1 - e->cur];
+    timed = timed && e->timing;
+    size_t ev = 0;
+    if (timed) {
+        if (s.tused + 2 > s.tev.size()) {
+            for (int j = 0; j < 2; ++j) {
+                hipEvent_t x;
+                HIPCHK(hipEventCreate(&x));
+                s.tev.push_back(x);
+            }
+        }
+        ev = s.tused;
+        s.tused += 2;
+        HIPCHK(hipEventRecord(s.tev[ev], s.stream));
+    }
+    if (e->band)
+        HIPCHK(golk_band_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->band_dw, e->strip, slots, s.err,
+                              s.stream));
+    else
+        HIPCHK(golk_bits_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->dw, e->strip, slots, s.stream));
+    if (timed) {
+        HIPCHK(hipEventRecord(s.tev[ev + 1], s.stream));
+        e->timed.push_back({i, ev, (double)rows * (double)e->W * k});
+    }
+    return GOL_OK;
+}
+
+// k turns of every shard: halo exchange, the interior rows [k, R-k) (they need no halo, so
+// they overlap the exchange), then the boundary rows once the halo is in.  With `count` the
+// alive cells of the output are added to each shard's slots.
+static int launch_k(gol_engine *e, int k, bool count)
+{
+    RCCHK(exchange(e, k));
+    const int n = (int)e->sh.size();
+    for (int i = 0; i < n; ++i) {
+        gol_shard &s = e->sh[i];
+        RCCHK(set_dev(s.device));
+        uint64_t *slots = count ? s.slots : nullptr;
+        if (count) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        if (e->transport == GOL_TRANSPORT_LOCAL) {
+            RCCHK(shard_kernel(e, i, k, 0, s.R, slots, true));
+            continue;
+        }
+        const bool interior = s.R >= 3 * k;
+        if (interior) RCCHK(shard_kernel(e, i, k, k, s.R - 2 * k, slots, true));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_comm, 0));
+        if (e->transport == GOL_TRANSPORT_LOOPBACK && n > 1) {
+            // the neighbours copy from my rows: my next launch (which overwrites them) waits
+            HIPCHK(hipStreamWaitEvent(s.stream, e->sh[(i + n - 1) % n].ev_comm, 0));
+            HIPCHK(hipStreamWaitEvent(s.stream, e->sh[(i + 1) % n].ev_comm, 0));
+        }
+        if (interior) {
+            RCCHK(shard_kernel(e, i, k, 0, k, slots, false));
+            RCCHK(shard_kernel(e, i, k, s.R - k, k, slots, false));
+        } else {
+            RCCHK(shard_kernel(e, i, k, 0, s.R, slots, true));
+        }
+    }
+    e->cur = 1 - e->cur;
+    return GOL_OK;
+}
+
+// Turn 1 of a board loaded with bytes other than 0/255 (worker.go:26-37): every shard runs the
+// exact byte kernel over its R rows plus the two halo rows it loaded, then packs the result.
+static int exact_turn(gol_engine *e)
+{
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(golk_bytes_step(s.bytes[0], s.R + 2, e->W, e->bstride, 1, s.R + 1, s.bytes[1], e->bstride, s.stream));
+        HIPCHK(golk_pack(s.bytes[1], s.R, e->W, e->bstride, s.bits[0], e->pitch, nullptr, s.stream));
+    }
+    e->cur = 0;
+    e->band = false;
+    e->mode = GOL_MODE_BITS;
+    return GOL_OK;
+}
+
+// Alive count of the current board into each shard's slots (zeroed first).
+static int count_into_slots(gol_engine *e)
+{
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        if (e->mode == GOL_MODE_BITS)
+            HIPCHK(golk_popcount(s.bits[e->cur], s.R, e->Wd, e->pitch, s.slots, s.stream));
+        else if (e->mode == GOL_MODE_EXACT)
+            HIPCHK(golk_count_bytes(s.bytes[0] + e->bstride, s.R, e->W, e->bstride, s.slots, s.stream));
+        else
+            HIPCHK(golk_count_bytes(s.bytes[e->bcur], e->H, e->W, e->bstride, s.slots, s.stream));
+    }
+    return GOL_OK;
+}
+
+// Advance n turns; with ci >= 0 store the alive count after them in every shard's counts[ci].
+static int advance(gol_engine *e, int64_t n, int64_t ci)
+{
+    bool counted = false;  // the last launch fused the count
+    while (n > 0) {
+        counted = false;
+        if (e->mode == GOL_MODE_EXACT) {
+            RCCHK(exact_turn(e));
+            e->turn += 1;
+            n -= 1;
+            continue;
+        }
+        if (e->mode == GOL_MODE_BYTES) {  // W % 64 != 0: one shard, the byte board
+            gol_shard &s = e->sh[0];
+            RCCHK(set_dev(s.device));
+            const uint8_t *mid = s.bytes[e->bcur];
+            if (e->bytes_binary && e->W % 32 == 0) {
+                // 0/255 byte board: k turns per launch on the bytes (torus wrap through top/bot)
+                const int k = e->k >= 32 && n >= 32 && e->H >= 32 ? 32 : pick_k(e->k, n, e->H, 1, false);
+                const bool last = n == k && ci >= 0;
+                if (last) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+                HIPCHK(golk_bytes_blocked(mid + (e->H - k) * e->bstride, mid, mid, s.bytes[1 - e->bcur], e->H, e->W,
+                                          e->bstride, 0, e->H, k, e->strip, last ? s.slots : nullptr, s.err, s.stream));
+                e->bcur = 1 - e->bcur;
+                e->turn += k;
+                n -= k;
+                counted = last;
+                continue;
+            }
+            HIPCHK(golk_bytes_step(mid, e->H, e->W, e->bstride, 0, e->H, s.bytes[1 - e->bcur], e->bstride, s.stream));
+            e->bcur = 1 - e->bcur;
+            e->bytes_binary = true;  // one exact turn leaves only 0/255
+            e->turn += 1;
+            n -= 1;
+            continue;
+        }
+        if (e->band_capable) RCCHK(convert(e, true));
+        const int k = pick_k(e->k, n, e->min_rows, e->band ? e->band_dw : e->dw, e->band);
+        const bool last = n == k && ci >= 0;
+        RCCHK(launch_k(e, k, last));
+        e->turn += k;
+        n -= k;
+        counted = last;
+    }
+    if (ci >= 0) {
+        if (!counted) RCCHK(count_into_slots(e));
+        for (auto &s : e->sh) {
+            RCCHK(set_dev(s.device));
+            HIPCHK(golk_slots_reduce(s.slots, 1, s.counts + ci, s.stream));
+        }
+    }
+    return GOL_OK;
+}
+
+int gol_engine_step_async(gol_engine *e, int64_t turns) { return advance(e, turns, -1); }
+
+extern "C" int gol_engine_step(gol_engine *e, int64_t turns)
+{
+    if (!e || turns < 0) return gol_set_error(GOL_EINVAL, "bad step arguments");
+    const int rc = advance(e, turns, -1);
+    const int rs = sync_all(e);
+    return rc ? rc : rs;
+}
+
+// Per-shard counts[0..n) -> the whole board's counts (host sum over local shards, RCCL sum
+// over the ranks of other processes).
+static int collect_counts(gol_engine *e, int64_t n, uint64_t *out)
+{
+    std::vector<uint64_t> tmp(e->sh.size() * n);
+    for (size_t i = 0; i < e->sh.size(); ++i) {
+        gol_shard &s = e->sh[i];
+        RCCHK(set_dev(s.device));
+        if (e->rank_mode && e->nranks > 1)
+            NCCLCHK(ncclAllReduce(s.counts, s.counts, n, ncclUint64, ncclSum, s.nccl, s.stream));
+        HIPCHK(hipMemcpyAsync(tmp.data() + i * n, s.counts, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream));
+    }
+    RCCHK(sync_all(e));
+    for (int64_t j = 0; j < n; ++j) {
+        uint64_t v = 0;
+        for (size_t i = 0; i < e->sh.size(); ++i) v += tmp[i * n + j];
+        out[j] = v;
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t every, uint64_t *counts, int64_t cap)
+{
+    if (!e || turns < 0 || every <= 0 || (turns / every > 0 && (!counts || cap < turns / every)))
+        return gol_set_error(GOL_EINVAL, "bad step_counted arguments (turns %lld, every %lld, cap %lld)", (long long)turns,
+                             (long long)every, (long long)cap);
+    const int64_t n = turns / every;
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(ensure_counts(s, n));
+    }
+    int rc = GOL_OK;
+    int64_t left = turns, ci = 0;
+    while (left > 0 && rc == GOL_OK) {
+        const int64_t seg = std::min(every, left);
+        rc = advance(e, seg, seg == every ? ci : -1);
+        if (seg == every) ++ci;
+        left -= seg;
+    }
+    if (rc != GOL_OK) {
+        (void)sync_all(e);
+        return rc;
+    }
+    if (n == 0) return sync_all(e);
+    return collect_counts(e, n, counts);
+}
+
+extern "C" int gol_engine_turn(gol_engine *e, int64_t *turn)
+{
+    if (!e || !turn) return gol_set_error(GOL_EINVAL, "bad arguments");
+    *turn = e->turn;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_alive_count(gol_engine *e, uint64_t *count)
+{
+    if (!e || !count) return gol_set_error(GOL_EINVAL, "bad arguments");
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(ensure_counts(s, 1));
+    }
+    RCCHK(count_into_slots(e));
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(golk_slots_reduce(s.slots, 1, s.counts, s.stream));
+    }
+    return collect_counts(e, 1, count);
+}
+
+extern "C" int gol_engine_hash(gol_engine *e, uint64_t *hash)
+{
+    if (!e || !hash) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "hash needs W %% 64 == 0");
+    RCCHK(ensure_standard(e));
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(ensure_counts(s, 1));
+        HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        const uint32_t *bits = s.bits[e->cur];
+        if (e->mode == GOL_MODE_EXACT) {  // loaded non-binary bytes at turn 0: hash the 255-cells
+            HIPCHK(golk_pack(s.bytes[0] + e->bstride, s.R, e->W, e->bstride, s.bits[0], e->pitch, nullptr, s.stream));
+            bits = s.bits[0];
+        }
+        HIPCHK(golk_hash(bits, s.R, s.y0, e->Wd, e->pitch, s.slots, s.stream));
+        HIPCHK(golk_slots_reduce(s.slots, 1, s.counts, s.stream));
+    }
+    return collect_counts(e, 1, hash);
+}
+
+// ------------------------------------------------------------------ load
+// Rows [y, y+n) of shard s (global rows) from host rows `src` (pitch `stride`) into the bit
+// board, through the staging buffer; ORs a nonbinary flag into s.flag.
+static int pack_rows_from_host(gol_engine *e, gol_shard &s, int64_t y, int64_t n, const uint8_t *src, int64_t stride)
+{
+    HIPCHK(hipMemcpy2DAsync(s.staging, e->bstride, src, stride, e->W, n, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(golk_pack(s.staging, n, e->W, e->bstride, s.bits[0] + (y - s.y0) * e->pitch, e->pitch, s.flag, s.stream));
+    return GOL_OK;
+}
+
+// After the bit rows of every shard were packed with s.flag set on bytes other than 0/255:
+// the global decision (every shard, every rank) whether turn 1 must run on the bytes.
+static int any_nonbinary(gol_engine *e, bool *out)
+{
+    uint32_t f = 0;
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        if (e->rank_mode && e->nranks > 1) NCCLCHK(ncclAllReduce(s.flag, s.flag, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+        HIPCHK(hipMemcpyAsync(s.host_word + 1, s.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+    }
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        f |= s.host_word[1];
+    }
+    *out = f != 0;
+    return GOL_OK;
+}
+
+static int alloc_exact_bytes(gol_engine *e, gol_shard &s)
+{
+    free_exact_bytes(s);
+    HIPCHK(hipMalloc(&s.bytes[0], (s.R + 2) * e->bstride));
+    HIPCHK(hipMalloc(&s.bytes[1], s.R * e->bstride));
+    return GOL_OK;
+}
+
+static void reset_board_state(gol_engine *e)
+{
+    e->turn = 0;
+    e->band = false;
+    e->cur = 0;
+    e->bcur = 0;
+}
+
+extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_t stride)
+{
+    if (!e || !world || stride < e->W) return gol_set_error(GOL_EINVAL, "bad load arguments");
+    reset_board_state(e);
+    if (e->mode == GOL_MODE_BYTES || !e->bit_capable) {  // one shard, byte board
+        gol_shard &s = e->sh[0];
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemcpy2DAsync(s.bytes[0], e->bstride, world, stride, e->W, e->H, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemsetAsync(s.flag, 0, sizeof(uint32_t), s.stream));
+        HIPCHK(golk_nonbinary(s.bytes[0], e->H, e->W, e->bstride, s.flag, s.stream));
+        HIPCHK(hipMemcpyAsync(s.host_word + 1, s.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        e->bytes_binary = s.host_word[1] == 0;
+        e->mode = GOL_MODE_BYTES;
+        return GOL_OK;
+    }
+    // pack each shard's rows into its bit board, noting bytes other than 0 / 255
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(ensure_staging(e, s));
+        HIPCHK(hipMemsetAsync(s.flag, 0, sizeof(uint32_t), s.stream));
+        for (int64_t y = s.y0; y < s.y1; y += s.stage_rows) {
+            const int64_t n = std::min(s.stage_rows, s.y1 - y);
+            RCCHK(pack_rows_from_host(e, s, y, n, world + y * stride, stride));
+        }
+    }
+    bool nonbinary = false;
+    RCCHK(any_nonbinary(e, &nonbinary));
+    if (!nonbinary) {
+        for (auto &s : e->sh) free_exact_bytes(s);
+        e->mode = GOL_MODE_BITS;
+        return GOL_OK;
+    }
+    // exact first turn (worker.go:26-37) needs the bytes: every shard keeps rows y0-1 .. y1
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(alloc_exact_bytes(e, s));
+        const int64_t above = (s.y0 + e->H - 1) % e->H, below = s.y1 % e->H;
+        HIPCHK(hipMemcpyAsync(s.bytes[0], world + above * stride, e->W, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemcpy2DAsync(s.bytes[0] + e->bstride, e->bstride, world + s.y0 * stride, stride, e->W, s.R,
+                                hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemcpyAsync(s.bytes[0] + (s.R + 1) * e->bstride, world + below * stride, e->W, hipMemcpyHostToDevice,
+                              s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+    }
+    e->mode = GOL_MODE_EXACT;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "random boards need W %% 64 == 0");
+    reset_board_state(e);
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        free_exact_bytes(s);
+        HIPCHK(golk_random_fill(s.bits[0], s.R, s.y0, e->W, e->pitch, seed, s.stream));
+    }
+    e->mode = GOL_MODE_BITS;
+    return sync_all(e);
+}
+
+// readPgmImage header (gol/io.go:97-117): fields = strings.Fields(data): "P5", width, height,
+// maxval; the raster is fields[4], i.e. it starts at the first non-space byte after maxval.
+static bool is_space(uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+static int parse_pgm_header(const uint8_t *h, size_t n, int64_t W, int64_t H, int64_t *off)
+{
+    std::string f[4];
+    size_t i = 0;
+    int nf = 0;
+    while (nf < 4) {
+        while (i < n && is_space(h[i])) ++i;
+        size_t j = i;
+        while (j < n && !is_space(h[j])) ++j;
+        if (j == i) break;
+        f[nf++] = std::string((const char *)h + i, j - i);
+        i = j;
+    }
+    if (nf < 1 || f[0] != "P5") return gol_set_error(GOL_EFORMAT, "Not a pgm file");
+    if (nf < 4) return gol_set_error(GOL_EFORMAT, "Not a pgm file");
+    if (atoll(f[1].c_str()) != W) return gol_set_error(GOL_EFORMAT, "Incorrect width");
+    if (atoll(f[2].c_str()) != H) return gol_set_error(GOL_EFORMAT, "Incorrect height");
+    if (atoll(f[3].c_str()) != 255) return gol_set_error(GOL_EFORMAT, "Incorrect maxval/bit depth");
+    while (i < n && is_space(h[i])) ++i;
+    if (i >= n) return gol_set_error(GOL_EFORMAT, "no pixel data after the header");
+    *off = (int64_t)i;
+    return GOL_OK;
+}
+
+static int pread_all(int fd, void *buf, size_t n, int64_t off)
+{
+    uint8_t *p = (uint8_t *)buf;
+    while (n > 0) {
+        const ssize_t r = pread(fd, p, n, off);
+        if (r <= 0) return gol_set_error(GOL_EIO, "short read at offset %lld", (long long)off);
+        p += r;
+        n -= (size_t)r;
+        off += r;
+    }
+    return GOL_OK;
+}
+
+// Stream rows [y, y+n) of the raster (at file offset `data`) through pinned staging.
+struct FileRows {
+    int fd;
+    int64_t data, W;
+};
+
+static int load_pgm_impl(gol_engine *e, const FileRows &fr)
+{
+    reset_board_state(e);
+    if (e->mode == GOL_MODE_BYTES || !e->bit_capable) {  // one shard, small byte board
+        std::vector<uint8_t> all(e->H * e->W);
+        RCCHK(pread_all(fr.fd, all.data(), all.size(), fr.data));
+        for (uint8_t c : all)
+            if (is_space(c)) return gol_set_error(GOL_EFORMAT, "pixel data shorter than W*H (a whitespace byte ends the field)");
+        return gol_engine_load_bytes(e, all.data(), e->W);
+    }
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(ensure_staging(e, s));
+        HIPCHK(hipMemsetAsync(s.flag, 0, sizeof(uint32_t), s.stream));
+        for (int64_t y = s.y0; y < s.y1; y += s.stage_rows) {
+            const int64_t n = std::min(s.stage_rows, s.y1 - y);
+            HIPCHK(hipStreamSynchronize(s.stream));  // the pinned rows are free again
+            RCCHK(pread_all(fr.fd, s.host_staging, (size_t)(n * e->W), fr.data + y * e->W));
+            RCCHK(pack_rows_from_host(e, s, y, n, s.host_staging, e->W));
+        }
+    }
+    bool nonbinary = false;
+    RCCHK(any_nonbinary(e, &nonbinary));
+    if (!nonbinary) {
+        e->mode = GOL_MODE_BITS;
+        return GOL_OK;
+    }
+    // bytes other than 0/255: check for whitespace bytes (the reference's strings.Fields
+    // split would end the raster there), then keep rows y0-1 .. y1 for the exact first turn
+    uint32_t ws = 0;
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(alloc_exact_bytes(e, s));
+        for (int64_t i = -1; i < s.R + 1; i += s.stage_rows) {
+            const int64_t n = std::min(s.stage_rows, s.R + 1 - i);
+            HIPCHK(hipStreamSynchronize(s.stream));
+            for (int64_t r = 0; r < n; ++r) {
+                const int64_t gy = ((s.y0 + i + r) % e->H + e->H) % e->H;
+                uint8_t *row = s.host_staging + r * e->W;
+                RCCHK(pread_all(fr.fd, row, (size_t)e->W, fr.data + gy * e->W));
+                if (i + r >= 0 && i + r < s.R)
+                    for (int64_t x = 0; x < e->W; ++x) ws |= is_space(row[x]);
+            }
+            HIPCHK(hipMemcpy2DAsync(s.bytes[0] + (i + 1) * e->bstride, e->bstride, s.host_staging, e->W, e->W, n,
+                                    hipMemcpyHostToDevice, s.stream));
+        }
+        HIPCHK(hipStreamSynchronize(s.stream));
+    }
+    if (e->rank_mode && e->nranks > 1) {  // agree on the verdict
+        gol_shard &s = e->sh[0];
+        s.host_word[2] = ws;
+        HIPCHK(hipMemcpyAsync(s.flag, s.host_word + 2, sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
+        NCCLCHK(ncclAllReduce(s.flag, s.flag, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+        HIPCHK(hipMemcpyAsync(s.host_word + 2, s.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        ws = s.host_word[2];
+    }
+    if (ws) {
+        for (auto &s : e->sh) free_exact_bytes(s);
+        return gol_set_error(GOL_EFORMAT, "pixel data shorter than W*H (a whitespace byte ends the field)");
+    }
+    e->mode = GOL_MODE_EXACT;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_load_pgm(gol_engine *e, const char *path)
+{
+    if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return gol_set_error(GOL_EIO, "cannot open %s", path);
+    uint8_t head[4096];
+    const ssize_t got = pread(fd, head, sizeof head, 0);
+    struct stat st;
+    int64_t off = 0;
+    int rc = got > 0 ? parse_pgm_header(head, (size_t)got, e->W, e->H, &off) : gol_set_error(GOL_EFORMAT, "Not a pgm file");
+    if (rc == GOL_OK && (fstat(fd, &st) != 0 || st.st_size < off + e->H * e->W))
+        rc = gol_set_error(GOL_EFORMAT, "pixel data shorter than W*H");
+    if (rc == GOL_OK) rc = load_pgm_impl(e, FileRows{fd, off, e->W});
+    close(fd);
+    return rc;
+}
+
+// ------------------------------------------------------------------ store / list / PGM
+// Rows [a, b) (global) of shard s as bytes into host `out` (pitch stride), chunked.
+static int shard_rows_to_host(gol_engine *e, gol_shard &s, int64_t a, int64_t b, uint8_t *out, int64_t stride)
+{
+    RCCHK(set_dev(s.device));
+    if (e->mode == GOL_MODE_BYTES) {
+        HIPCHK(hipMemcpy2DAsync(out, stride, s.bytes[e->bcur] + a * e->bstride, e->bstride, e->W, b - a,
+                                hipMemcpyDeviceToHost, s.stream));
+    } else if (e->mode == GOL_MODE_EXACT) {
+        HIPCHK(hipMemcpy2DAsync(out, stride, s.bytes[0] + (1 + a - s.y0) * e->bstride, e->bstride, e->W, b - a,
+                                hipMemcpyDeviceToHost, s.stream));
+    } else {
+        RCCHK(ensure_staging(e, s));
+        for (int64_t y = a; y < b; y += s.stage_rows) {
+            const int64_t n = std::min(s.stage_rows, b - y);
+            HIPCHK(golk_unpack(s.bits[e->cur] + (y - s.y0) * e->pitch, n, e->W, e->pitch, s.staging, e->bstride, s.stream));
+            HIPCHK(hipMemcpy2DAsync(out + (y - a) * stride, stride, s.staging, e->bstride, e->W, n, hipMemcpyDeviceToHost,
+                                    s.stream));
+        }
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_store_rows(gol_engine *e, int64_t y0, int64_t y1, uint8_t *out, int64_t stride)
+{
+    if (!e || !out || stride < e->W || y0 < 0 || y1 > e->H || y0 > y1) return gol_set_error(GOL_EINVAL, "bad store arguments");
+    if (y0 < e->sh.front().y0 || y1 > e->sh.back().y1)
+        return gol_set_error(GOL_EINVAL, "rows [%lld, %lld) are not held by this process (rows [%lld, %lld))", (long long)y0,
+                             (long long)y1, (long long)e->sh.front().y0, (long long)e->sh.back().y1);
+    RCCHK(ensure_standard(e));
+    for (auto &s : e->sh) {
+        const int64_t a = std::max(y0, s.y0), b = std::min(y1, s.y1);
+        if (a < b) RCCHK(shard_rows_to_host(e, s, a, b, out + (a - y0) * stride, stride));
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t stride)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    return gol_engine_store_rows(e, 0, e->H, out, stride);
+}
+
+// Row-major (x, y) list of the cells of rows [0, rows) of `board` (global row gy0) that are
+// alive (prev == NULL) or whose alive state differs from `prev`: per-row counts -> host
+// exclusive scan -> one wave per row.  Writes min(total, cap) pairs, *n = total.
+static int list_cells(gol_engine *e, gol_shard &s, bool bm, const void *board, const void *prev, int64_t rows,
+                      int64_t units, int64_t pitch, int64_t gy0, int32_t *xy, int64_t cap, int64_t *n)
+{
+    RCCHK(set_dev(s.device));
+    int64_t *dcounts = nullptr;
+    int32_t *dxy = nullptr;
+    std::vector<int64_t> counts(std::max<int64_t>(rows, 1));
+    HIPCHK(hipMalloc(&dcounts, counts.size() * sizeof(int64_t)));
+    hipError_t he = golk_row_counts(bm, board, prev, rows, units, pitch, dcounts, s.stream);
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(counts.data(), dcounts, rows * sizeof(int64_t), hipMemcpyDeviceToHost, s.stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(s.stream);
+    int64_t total = 0;
+    if (he == hipSuccess) {
+        for (int64_t y = 0; y < rows; ++y) {  // exclusive prefix -> first index of each row
+            const int64_t v = counts[y];
+            counts[y] = total;
+            total += v;
+        }
+        *n = total;
+    }
+    const int64_t m = std::min(total, cap);
+    if (he == hipSuccess && m > 0) {
+        he = hipMemcpyAsync(dcounts, counts.data(), rows * sizeof(int64_t), hipMemcpyHostToDevice, s.stream);
+        if (he == hipSuccess) he = hipMalloc(&dxy, m * 2 * sizeof(int32_t));
+        if (he == hipSuccess) he = golk_alive_list(bm, board, prev, rows, units, pitch, dcounts, dxy, m, gy0, s.stream);
+        if (he == hipSuccess) he = hipMemcpyAsync(xy, dxy, m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(s.stream);
+    }
+    (void)hipFree(dcounts);
+    if (dxy) (void)hipFree(dxy);
+    if (he != hipSuccess) return gol_set_error(GOL_EHIP, "cell list: %s", hipGetErrorString(he));
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
+{
+    if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
+    RCCHK(ensure_standard(e));
+    int64_t total = 0;
+    for (auto &s : e->sh) {
+        int64_t got = 0;
+        const int64_t room = std::max<int64_t>(0, cap - total);
+        int32_t *dst = room > 0 ? xy + 2 * total : nullptr;
+        if (e->mode == GOL_MODE_BITS)
+            RCCHK(list_cells(e, s, true, s.bits[e->cur], nullptr, s.R, e->Wd, e->pitch, s.y0, dst, room, &got));
+        else if (e->mode == GOL_MODE_EXACT)
+            RCCHK(list_cells(e, s, false, s.bytes[0] + e->bstride, nullptr, s.R, e->W, e->bstride, s.y0, dst, room, &got));
+        else
+            RCCHK(list_cells(e, s, false, s.bytes[e->bcur], nullptr, e->H, e->W, e->bstride, 0, dst, room, &got));
+        total += got;
+    }
+    *n = total;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
+{
+    if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
+    RCCHK(ensure_standard(e));
+    int64_t total = 0;
+    if (e->mode == GOL_MODE_BITS) {
+        // one standard-layout turn; the previous generation stays in the other buffer
+        RCCHK(launch_k(e, 1, false));
+        e->turn += 1;
+        RCCHK(sync_all(e));
+        for (auto &s : e->sh) {
+            int64_t got = 0;
+            const int64_t room = std::max<int64_t>(0, cap - total);
+            RCCHK(list_cells(e, s, true, s.bits[e->cur], s.bits[1 - e->cur], s.R, e->Wd, e->pitch, s.y0,
+                             room > 0 ? xy + 2 * total : nullptr, room, &got));
+            total += got;
+        }
+        *n = total;
+        return GOL_OK;
+    }
+    if (e->mode == GOL_MODE_EXACT) {
+        // turn 1 from the loaded bytes: compare the new state (unpacked) with the loaded bytes
+        RCCHK(exact_turn(e));
+        e->turn += 1;
+        for (auto &s : e->sh) {
+            RCCHK(set_dev(s.device));
+            HIPCHK(golk_unpack(s.bits[e->cur], s.R, e->W, e->pitch, s.bytes[1], e->bstride, s.stream));
+        }
+        for (auto &s : e->sh) {
+            int64_t got = 0;
+            const int64_t room = std::max<int64_t>(0, cap - total);
+            RCCHK(list_cells(e, s, false, s.bytes[1], s.bytes[0] + e->bstride, s.R, e->W, e->bstride, s.y0,
+                             room > 0 ? xy + 2 * total : nullptr, room, &got));
+            total += got;
+        }
+        *n = total;
+        return sync_all(e);  // frees the byte rows
+    }
+    // byte board (W % 64 != 0): one shard; the previous bytes stay in the other buffer
+    RCCHK(advance(e, 1, -1));
+    RCCHK(sync_all(e));
+    gol_shard &s = e->sh[0];
+    RCCHK(list_cells(e, s, false, s.bytes[e->bcur], s.bytes[1 - e->bcur], e->H, e->W, e->bstride, 0, xy, cap, &total));
+    *n = total;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
+{
+    if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
+    RCCHK(ensure_standard(e));
+    char header[96];
+    const int hlen = snprintf(header, sizeof header, "P5\n%lld %lld\n255\n", (long long)e->W, (long long)e->H);  // io.go:52-59
+    const bool several = e->rank_mode && e->nranks > 1;
+    int rc = GOL_OK;
+    if (!several || e->rank == 0) {
+        const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) rc = gol_set_error(GOL_EIO, "cannot create %s", path);
+        else {
+            if (write(fd, header, hlen) != hlen) rc = gol_set_error(GOL_EIO, "short write to %s", path);
+            else if (several && ftruncate(fd, hlen + e->H * e->W) != 0) rc = gol_set_error(GOL_EIO, "cannot size %s", path);
+            if (close(fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
+        }
+    }
+    if (several) {
+        const int rb = rank_barrier(e);  // the file exists and is sized before any rank writes
+        if (rc == GOL_OK) rc = rb;
+    }
+    const int fd = rc == GOL_OK ? open(path, O_WRONLY) : -1;
+    if (rc == GOL_OK && fd < 0) rc = gol_set_error(GOL_EIO, "cannot open %s", path);
+    for (auto &s : e->sh) {
+        if (rc != GOL_OK) break;
+        rc = set_dev(s.device);
+        if (rc == GOL_OK) rc = ensure_staging(e, s);
+        const int64_t r0 = e->mode == GOL_MODE_BYTES ? 0 : s.y0, r1 = e->mode == GOL_MODE_BYTES ? e->H : s.y1;
+        for (int64_t y = r0; y < r1 && rc == GOL_OK; y += s.stage_rows) {
+            const int64_t n = std::min(s.stage_rows, r1 - y);
+            rc = shard_rows_to_host(e, s, y, y + n, s.host_staging, e->W);
+            const size_t bytes = (size_t)(n * e->W);
+            if (rc == GOL_OK && pwrite(fd, s.host_staging, bytes, hlen + y * e->W) != (ssize_t)bytes)
+                rc = gol_set_error(GOL_EIO, "short write to %s", path);
+        }
+    }
+    if (fd >= 0 && close(fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
+    if (several) {
+        const int rb = rank_barrier(e);  // every rank's rows are written when any rank returns
+        if (rc == GOL_OK) rc = rb;
+    }
+    return rc;
+}
+
+// ------------------------------------------------------------------ info
+extern "C" int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lane, int32_t *strip_rows,
+                               int32_t *bit_mode)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    const bool bits = e->mode == GOL_MODE_BITS;
+    const bool band = bits && e->band_capable;
+    const int dw = band ? e->band_dw : e->dw;
+    const int kk = pick_k(e->k, e->k, e->min_rows, dw, band);
+    if (k) *k = kk;
+    if (cells_per_lane) *cells_per_lane = 32 * dw;
+    if (strip_rows) {
+        const int64_t u = band ? golk_band_useful_words(kk, dw) : 62 * dw;
+        const int64_t ng = (e->Wd + u - 1) / u;
+        *strip_rows = e->strip > 0 ? e->strip : golk_auto_strip(e->min_rows, ng, kk);
+    }
+    if (bit_mode) *bit_mode = bits ? (band ? 2 : 1) : 0;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *pitch)
+{
+    if (!e || !bits || !pitch) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (e->mode != GOL_MODE_BITS) return gol_set_error(GOL_ESTATE, "board is not bit-resident");
+    RCCHK(ensure_standard(e));
+    RCCHK(sync_all(e));
+    *bits = e->sh[0].bits[e->cur];
+    *pitch = e->pitch;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_set_timing(gol_engine *e, int32_t enable)
+{
+    if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    e->timing = enable != 0;
+    e->timed.clear();
+    for (auto &s : e->sh) s.tused = 0;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double *mean_cell_updates)
+{
+    if (!e || !launches || !mean_ms || !mean_cell_updates) return gol_set_error(GOL_EINVAL, "bad arguments");
+    RCCHK(sync_all(e));
+    double ms = 0, cells = 0;
+    for (const auto &t : e->timed) {
+        gol_shard &s = e->sh[t.shard];
+        RCCHK(set_dev(s.device));
+        float x = 0;
+        HIPCHK(hipEventElapsedTime(&x, s.tev[t.ev], s.tev[t.ev + 1]));
+        ms += x;
+        cells += t.cell_updates;
+    }
+    const int64_t n = (int64_t)e->timed.size();
+    *launches = n;
+    *mean_ms = n ? ms / n : 0.0;
+    *mean_cell_updates = n ? cells / n : 0.0;
+    return GOL_OK;
+}

@@ -98,6 +98,9 @@ struct Operations {
         if (eng) gol_engine_destroy(eng);
     }
 
+    // The board of a Run: row-sharded over cfg.shards GPUs (broker.go:135-206's split applied
+    // to GPUs) when configured and the board allows it (W % 64 == 0, at least one row per
+    // shard), else on one GPU.
     int ensure_engine(int64_t h, int64_t w)
     {
         if (eng && H == h && W == w) return GOL_OK;
@@ -105,7 +108,10 @@ struct Operations {
         eng = nullptr;
         H = h;
         W = w;
-        return gol_engine_create(h, w, &cfg, &eng);
+        gol_config c = cfg;
+        if (c.shards > 1 && (w % 64 != 0 || h < c.shards)) c.shards = 1;
+        if (c.shards <= 1) c.transport = GOL_TRANSPORT_AUTO;
+        return gol_engine_create(h, w, &c, &eng);
     }
 
     // Turn-loop control point (broker.go:79-88 / 122-130), checked between steps.

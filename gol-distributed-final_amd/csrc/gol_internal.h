@@ -1,56 +1,91 @@
 // gol_internal.h -- private state of libgolhip.so (not part of the C ABI).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdarg.h>
 #include <stdint.h>
+
+#include <vector>
 
 #include "golhip.h"
 
 // Library defaults for the bit-board step (chosen from the gfx950 sweep recorded
 // in DESIGN.md; overridable per engine through gol_config).
-#ifndef GOL_DEFAULT_K
 #define GOL_DEFAULT_K 8        // standard layout
-#endif
-#ifndef GOL_DEFAULT_BAND_K
 #define GOL_DEFAULT_BAND_K 12  // band layout, 4 words per lane: the split pipeline
-#endif
-#ifndef GOL_DEFAULT_DW
-#define GOL_DEFAULT_DW 2
-#endif
+#define GOL_DEFAULT_DW 2       // standard layout: 64 cells per lane
 
-// Halo rows kept above and below each bit buffer: the band kernel reads the torus wrap
-// from them as contiguous rows (its CONTIG path, no per-row segment select).
+// Ghost rows kept above and below each bit buffer: the halo (received from the neighbouring
+// shards, or the torus wrap of a single shard) lands there, contiguous with the shard's rows,
+// so the kernels address input row y as board + y*pitch for -k <= y < R + k.
 #define GOL_GHOST_ROWS 16
 
-struct gol_engine {
+// One row shard: rows [y0, y1) of the board on one GPU.
+struct gol_shard {
     int device = 0;
-    hipStream_t stream = nullptr;
+    int64_t y0 = 0, y1 = 0, R = 0;
+    hipStream_t stream = nullptr;  // kernels
+    hipStream_t comm = nullptr;    // halo exchange
+    hipEvent_t ev_ready = nullptr; // this shard's input board of the next launch is complete
+    hipEvent_t ev_comm = nullptr;  // this shard's halo exchange of the current launch is done
+    uint32_t *bits[2] = {nullptr, nullptr};        // row 0 of each bit buffer
+    uint32_t *bits_alloc[2] = {nullptr, nullptr};  // allocations incl. the ghost rows
+    // BYTES mode: the H x W byte board (double buffer).  EXACT mode: bytes[0] = rows
+    // y0-1 .. y1 (R + 2 rows, the halo rows from the host board), bytes[1] = R output rows.
+    uint8_t *bytes[2] = {nullptr, nullptr};
+    uint64_t *slots = nullptr;        // GOL_COUNT_SLOTS * 8 reduction slots
+    uint64_t *counts = nullptr;       // per-count-point alive counts (step_counted)
+    int64_t counts_cap = 0;
+    uint32_t *flag = nullptr;         // nonbinary flag of a load
+    uint32_t *err = nullptr;          // device error word of this shard's launches
+    uint32_t *host_word = nullptr;    // pinned readback of err / flag
+    uint8_t *staging = nullptr;       // device byte rows for chunked copies
+    uint8_t *host_staging = nullptr;  // pinned host rows
+    int64_t stage_rows = 0;
+    ncclComm_t nccl = nullptr;
+    // timing (gol_engine_set_timing): events on `stream` around the timed launches
+    std::vector<hipEvent_t> tev;
+    size_t tused = 0;
+};
+
+enum gol_mode {
+    GOL_MODE_BITS,   // bit board (W % 64 == 0)
+    GOL_MODE_BYTES,  // byte board: W % 64 != 0 (one shard)
+    GOL_MODE_EXACT   // bit-capable board loaded with bytes other than 0/255: turn 1 is exact
+};
+
+struct gol_timed {
+    int shard;
+    size_t ev;  // index of the start event in the shard's pool (stop = ev + 1)
+    double cell_updates;
+};
+
+struct gol_engine {
     int64_t H = 0, W = 0;
     int64_t Wd = 0;      // uint32 words per row (W / 32)
     int64_t pitch = 0;   // bit-board row pitch in uint32 words (multiple of 4)
     int64_t bstride = 0; // byte-board row pitch in bytes (multiple of 16)
+    std::vector<gol_shard> sh;
+    int nranks = 1;      // shards of the whole board
+    int rank = 0;        // global rank of sh[0] (local shards are consecutive ranks)
+    bool rank_mode = false;  // other ranks live in other processes
+    int transport = GOL_TRANSPORT_LOCAL;
+    int64_t min_rows = 0;    // rows of the smallest shard (the broker split: H / nranks)
     bool bit_capable = false;  // W % 64 == 0
-    bool bit_mode = false;     // board currently lives in bits[cur] (else bytes[bcur])
-    bool band_capable = false; // step the bit board in the band layout (W % 1024 == 0, not disabled)
-    bool band = false;         // bits[cur] currently holds the band layout
-    uint32_t *bits[2] = {nullptr, nullptr};       // row 0 of each bit buffer
-    uint32_t *bits_alloc[2] = {nullptr, nullptr}; // allocations: GOL_GHOST_ROWS halo rows above and below
-    int cur = 0;
-    uint8_t *bytes[2] = {nullptr, nullptr};
-    int bcur = 0;
-    bool bytes_binary = false;  // byte board holds only 0/255 (k-turn byte kernel allowed)
-    uint64_t *slots = nullptr;  // GOL_COUNT_SLOTS * 8 uint64 reduction slots
-    uint32_t *flag = nullptr;
-    uint8_t *staging = nullptr;       // device byte rows for chunked copies
-    uint8_t *host_staging = nullptr;  // pinned host rows (PGM writer)
-    int64_t stage_rows = 0;
+    bool band_capable = false; // step the bit board in the band layout
+    bool band = false;         // bits[cur] currently hold the band layout
+    gol_mode mode = GOL_MODE_BITS;
+    bool bytes_binary = false; // BYTES mode: the board holds only 0/255
+    int cur = 0, bcur = 0;
     int64_t turn = 0;
     int k = GOL_DEFAULT_K;
     int dw = GOL_DEFAULT_DW;
-    int band_dw = 4;  // words per lane of the band kernel
+    int band_dw = 4;
     int strip = 0;
+    bool timing = false;
+    std::vector<gol_timed> timed;
 };
 
 int gol_set_error(int code, const char *fmt, ...);
-// Enqueue `turns` turns on e->stream without synchronising.
-int gol_engine_step_async(gol_engine *e, int64_t turns, uint64_t *count_slots);
+// Enqueue `turns` turns on the shards' streams without synchronising.
+int gol_engine_step_async(gol_engine *e, int64_t turns);

@@ -7,28 +7,27 @@
 #define GOL_COUNT_SLOTS 256
 #endif
 
-#ifndef GOL_DEFAULT_ALGO
-#define GOL_DEFAULT_ALGO 1
-#endif
-int golk_bits_algo();
+// Flags of a launch's device error word (ORed by the failing waves).
+#define GOLK_ERR_SPIN 1u  // a pipeline wave gave up waiting for an LDS flag (protocol fault)
+
+// Per-device error word for launches made without one (lazily allocated, zeroed).
+uint32_t *golk_device_err_word(int device);
+
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k);
+// Standard layout: dw words per lane (1, 2 or 4), k in {1, 2, 4, 8} (and 16 for dw <= 2).
 hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
                           int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw,
                           int strip, uint64_t *slots, hipStream_t s);
-// Band layout (bit b of word w = cell b*Wd + w): dw words per lane (2 or 4), k in {1, 2, 4, 8}
-// (and 16 for dw = 2), Wd % dw == 0, pitch % dw == 0, 4*dw-byte aligned rows.
+// Band layout (bit b of word w = cell b*Wd + w): dw words per lane (2 or 4), k in {1, 2, 4, 8},
+// 16 for dw = 2, 12 for dw = 4 (the split pipeline); Wd % dw == 0, pitch % dw == 0, 4*dw-byte
+// aligned rows.  err: error word of the launch (NULL = the device's default word).
 #ifndef GOL_BAND_DEFAULT_DW
 #define GOL_BAND_DEFAULT_DW 4
 #endif
 hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
-                          uint64_t *slots, hipStream_t s);
+                          uint64_t *slots, uint32_t *err, hipStream_t s);
 int golk_band_useful_words(int k, int dw);
-// Split-pipeline band kernel: k = 8/12/16 as 2/3/4 waves x 4 stages.
-#ifndef GOL_BAND_SPLIT_DEFAULT
-#define GOL_BAND_SPLIT_DEFAULT 0
-#endif
-int golk_band_split_enabled();
 // Standard <-> band rows (Wd % 32 == 0), out of place.
 hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
                              int64_t spitch, int64_t dpitch, hipStream_t s);
@@ -36,12 +35,14 @@ hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t s
                            uint8_t *out, int64_t out_stride, hipStream_t s);
 hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst, int64_t R,
                               int64_t W, int64_t pitch, int64_t row0, int64_t rows, int k, int strip, uint64_t *slots,
-                              hipStream_t s);
+                              uint32_t *err, hipStream_t s);
 hipError_t golk_nonbinary(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *flag, hipStream_t s);
 hipError_t golk_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t W, int64_t pitch, uint64_t seed,
                             hipStream_t s);
 hipError_t golk_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots,
                          hipStream_t s);
+// out[i] = sum of the GOL_COUNT_SLOTS slots of slot array i (arrays of GOL_COUNT_SLOTS*8 uint64).
+hipError_t golk_slots_reduce(const uint64_t *slots, int64_t n, uint64_t *out, hipStream_t s);
 hipError_t golk_hash(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Wd, int64_t pitch, uint64_t *slots,
                      hipStream_t s);
 hipError_t golk_count_bytes(const uint8_t *src, int64_t rows, int64_t W, int64_t stride, uint64_t *slots,
@@ -51,8 +52,9 @@ hipError_t golk_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stri
 hipError_t golk_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes, int64_t stride,
                        hipStream_t s);
 // Per-row counts and the row-major (x, y) list of alive cells; with prev != NULL of the cells
-// whose alive state differs between board and prev (same layout and pitch).
+// whose alive state differs between board and prev (same layout and pitch).  y0 is added to
+// the listed y (global row of the first row).
 hipError_t golk_row_counts(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
                            int64_t pitch, int64_t *out, hipStream_t s);
 hipError_t golk_alive_list(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
-                           int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s);
+                           int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, int64_t y0, hipStream_t s);

@@ -4,27 +4,34 @@
 //   worker.go:15-42 calculateNextState, worker.go:44-70 calculateSurroundings
 //   broker.go:47-58 calculateAliveCells (count part)
 // with two board representations:
-//   * bit board  : 32 cells per uint32 (64 per uint64, LSB = lowest x).  One
-//                  lane owns DW consecutive words of a row and slides down a
-//                  strip of rows; K generations are pipelined in registers
-//                  (temporal blocking), so a launch reads and writes the board
-//                  once for K turns.
+//   * bit board  : 32 cells per uint32 (64 per uint64, LSB = lowest x).  A lane
+//                  owns DW consecutive words of a row and slides down a strip
+//                  of rows; K generations are pipelined in registers (temporal
+//                  blocking), so a launch reads and writes the board once for K
+//                  turns.  Stepped in the column-band layout (bit b of word w =
+//                  cell b*Wd + w, shift-free generations) when W % 1024 == 0.
 //   * byte board : one byte per cell (exact reference semantics incl. bytes
 //                  that are neither 0 nor 255), SWAR on 4 cells per VGPR.
-// No LDS and no barriers: neighbouring words move between lanes with DPP
-// wave_shr:1 / wave_shl:1; lanes 0 and 63 of every wave are halo lanes whose
-// results are discarded (the halo is one word = 32 cells >= K).
+// One compiled path per kernel family; the variants measured and dropped in
+// round 1 (vertical-first stages, barrier-synchronised split pipeline, centred
+// standard-layout stages, per-role profiling builds) are recorded in DESIGN.md
+// and live in git history (commit 297b13e).
 #include <hip/hip_runtime.h>
-#include <map>
-#include <mutex>
 #include <stdint.h>
-
 #include <stdlib.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "gol_kernels.h"
+
+// Polls of a pipeline flag before a wave gives up (sets GOLK_ERR_SPIN in the launch's error
+// word and leaves; the host turns that into GOL_EHIP).  A test build sets 0 to force the path.
+#ifndef GOL_SPIN_LIMIT
+#define GOL_SPIN_LIMIT (1 << 22)
+#endif
 
 namespace golk {
 
@@ -77,6 +84,12 @@ __device__ __forceinline__ void slot_add(uint64_t *slots, uint64_t v)
     }
 }
 
+// Error word of a launch: flags ORed by lane 0 of a failing wave (a vector global atomic).
+__device__ __forceinline__ void raise_error(uint32_t *err, uint32_t flag)
+{
+    if ((threadIdx.x & 63) == 0) atomicOr(err, flag);
+}
+
 template <int DW> struct VecT;
 template <> struct VecT<1> { typedef uint32_t type; };
 template <> struct VecT<2> { typedef uint2 type; };
@@ -102,27 +115,9 @@ __device__ __forceinline__ void store_words(uint32_t *p, const uint32_t (&w)[DW]
     *reinterpret_cast<V *>(p) = v;
 }
 
-// Horizontal 3-cell sums of one row (cell itself + left + right), bit-sliced:
-// value = h0 + 2*h1 in 0..3 per cell.
-template <int DW>
-__device__ __forceinline__ void hsum(const uint32_t (&c)[DW], uint32_t (&h0)[DW], uint32_t (&h1)[DW])
-{
-    const uint32_t left_in = from_lower_lane(c[DW - 1]);  // word to the left of c[0]
-    const uint32_t right_in = from_upper_lane(c[0]);      // word to the right of c[DW-1]
-#pragma unroll
-    for (int j = 0; j < DW; ++j) {
-        const uint32_t wl = (j == 0) ? left_in : c[j - 1];
-        const uint32_t wr = (j == DW - 1) ? right_in : c[j + 1];
-        const uint32_t L = __builtin_amdgcn_alignbit(c[j], wl, 31);  // cell x-1 at bit x
-        const uint32_t R = __builtin_amdgcn_alignbit(wr, c[j], 1);   // cell x+1 at bit x
-        h0[j] = bitop3<TT_XOR3>(L, c[j], R);
-        h1[j] = bitop3<TT_MAJ>(L, c[j], R);
-    }
-}
-
-// B3/S23 from three horizontal sums (rows above/middle/below) and the middle
-// cell.  T = sum of the 3x3 block including the cell = t0 + 2*(k0 + u + 2v);
-// alive' = (T == 3) | (cell & T == 4).
+// B3/S23 from three horizontal sums (rows above/middle/below, value = h0 + 2*h1 in 0..3 per
+// cell) and the middle cell.  T = sum of the 3x3 block including the cell = t0 + 2*(k0 + u +
+// 2v); alive' = (T == 3) | (cell & T == 4).
 __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
                                          uint32_t c0, uint32_t c1, uint32_t cell)
 {
@@ -135,10 +130,10 @@ __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, 
     return bitop3<TT_MUX>(t0, eq1, eq2 & cell);
 }
 
-// ------------------------------------------------------------------ bit-board step
-// Pipeline state of stage g (generation g+1): ring of 3 rows of horizontal sums
-// plus the cells of those rows.  Slot s = step % 3 holds the row received at
-// this step; the stage emits the next state of the row received one step ago.
+// ------------------------------------------------------------------ register pipeline
+// State of stage g (generation g+1): a ring of 3 rows of horizontal sums plus the cells of
+// those rows.  Slot s = step % 3 holds the row received at this step; the stage emits the
+// next state of the row received one step ago.
 template <int K, int DW>
 struct Pipe {
     uint32_t h0[K][3][DW];
@@ -146,33 +141,22 @@ struct Pipe {
     uint32_t cc[K][3][DW];
 };
 
-template <int K, int DW, int S>
-__device__ __forceinline__ void pipe_step(Pipe<K, DW> &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
+template <int K, int DW>
+__device__ __forceinline__ void pipe_init(Pipe<K, DW> &p)
 {
-    constexpr int SA = (S + 1) % 3;  // two rows back (above)
-    constexpr int SM = (S + 2) % 3;  // one row back (the row being emitted)
-    uint32_t cur[DW];
 #pragma unroll
-    for (int j = 0; j < DW; ++j) cur[j] = in[j];
+    for (int g = 0; g < K; ++g)
 #pragma unroll
-    for (int g = 0; g < K; ++g) {
+        for (int s = 0; s < 3; ++s)
 #pragma unroll
-        for (int j = 0; j < DW; ++j) p.cc[g][S][j] = cur[j];
-        hsum<DW>(p.cc[g][S], p.h0[g][S], p.h1[g][S]);
-#pragma unroll
-        for (int j = 0; j < DW; ++j)
-            cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j],
-                          p.h0[g][S][j], p.h1[g][S][j], p.cc[g][SM][j]);
-    }
-#pragma unroll
-    for (int j = 0; j < DW; ++j) out[j] = cur[j];
+            for (int j = 0; j < DW; ++j) { p.h0[g][s][j] = 0; p.h1[g][s][j] = 0; p.cc[g][s][j] = 0; }
 }
 
-// Shifted-frame variant: the horizontal 3-sum is formed from the cell and its
-// two LEFT neighbours, S'[p] = c[p] + c[p-1] + c[p-2] = the 3-sum centred on p-1,
-// so a stage needs one DPP (left word) instead of two and the centre cell is
-// c << 1.  Every generation moves the frame one bit to the left; after K
-// generations one funnel shift with the right neighbour word realigns the row.
+// Standard layout, shifted frame: the horizontal 3-sum is formed from the cell and its two
+// LEFT neighbours, S'[p] = c[p] + c[p-1] + c[p-2] = the 3-sum centred on p-1, so a stage
+// needs one DPP (left word) instead of two and the centre cell is c << 1.  Every
+// generation moves the frame one bit to the left; after K generations one funnel shift
+// with the right neighbour word realigns the row.
 template <int DW>
 __device__ __forceinline__ void hsum_left(const uint32_t (&c)[DW], uint32_t (&h0)[DW], uint32_t (&h1)[DW],
                                           uint32_t (&ctr)[DW])
@@ -189,39 +173,7 @@ __device__ __forceinline__ void hsum_left(const uint32_t (&c)[DW], uint32_t (&h0
     }
 }
 
-template <int K, int DW, int S>
-__device__ __forceinline__ void spipe_step(Pipe<K, DW> &p, const uint32_t (&in)[DW], uint32_t (&out)[DW])
-{
-    constexpr int SA = (S + 1) % 3;
-    constexpr int SM = (S + 2) % 3;
-    uint32_t cur[DW];
-#pragma unroll
-    for (int j = 0; j < DW; ++j) cur[j] = in[j];
-#pragma unroll
-    for (int g = 0; g < K; ++g) {
-        hsum_left<DW>(cur, p.h0[g][S], p.h1[g][S], p.cc[g][S]);
-#pragma unroll
-        for (int j = 0; j < DW; ++j)
-            cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j],
-                          p.h0[g][S][j], p.h1[g][S][j], p.cc[g][SM][j]);
-    }
-#pragma unroll
-    for (int j = 0; j < DW; ++j) out[j] = cur[j];
-}
-
-// One pipeline stage (generation g+1) of one row step S, in place on `cur`.
-template <int K, int DW, int S>
-__device__ __forceinline__ void hstage(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
-{
-    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
-#pragma unroll
-    for (int j = 0; j < DW; ++j) p.cc[g][S][j] = cur[j];
-    hsum<DW>(p.cc[g][S], p.h0[g][S], p.h1[g][S]);
-#pragma unroll
-    for (int j = 0; j < DW; ++j)
-        cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j], p.h0[g][S][j],
-                      p.h1[g][S][j], p.cc[g][SM][j]);
-}
+// One shifted-frame stage (generation g+1) of one row step S, in place on `cur`.
 template <int K, int DW, int S>
 __device__ __forceinline__ void sstage(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
 {
@@ -233,52 +185,20 @@ __device__ __forceinline__ void sstage(Pipe<K, DW> &p, const int g, uint32_t (&c
                       p.h1[g][S][j], p.cc[g][SM][j]);
 }
 
-template <int K, int DW, int ALGO> struct PipeSel;
-template <int K, int DW> struct PipeSel<K, DW, 0> {
-    typedef Pipe<K, DW> type;
-    static __device__ __forceinline__ void init(type &p)
-    {
-#pragma unroll
-        for (int g = 0; g < K; ++g)
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-#pragma unroll
-                for (int j = 0; j < DW; ++j) { p.h0[g][s][j] = 0; p.h1[g][s][j] = 0; p.cc[g][s][j] = 0; }
-    }
-    template <int S>
-    static __device__ __forceinline__ void stage(type &p, const int g, uint32_t (&cur)[DW])
-    {
-        hstage<K, DW, S>(p, g, cur);
-    }
-};
-template <int K, int DW> struct PipeSel<K, DW, 1> : PipeSel<K, DW, 0> {
-    typedef Pipe<K, DW> type;
-    template <int S>
-    static __device__ __forceinline__ void stage(type &p, const int g, uint32_t (&cur)[DW])
-    {
-        sstage<K, DW, S>(p, g, cur);
-    }
-};
-
 struct BitsArgs {
     const uint32_t *top, *mid, *bot;
     uint32_t *dst;
     int64_t R, Wd, pitch, row0, rows;
     int32_t strip, ngroups;
     uint64_t *slots;
+    uint32_t *err;
 };
 
-
+// ------------------------------------------------------------------ bit-board step, standard layout
 // grid.x: groups of 4 waves along the row; grid.y: strips of output rows.
 // Wave = one column group of 62*DW output words (+1 halo lane each side).
-// Occupancy floor for the register allocator (waves per SIMD); 1 = no constraint.
-#ifndef GOL_MIN_WAVES
-#define GOL_MIN_WAVES(K, DW) 1
-#endif
-
-template <int K, int DW, int ALGO>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_MIN_WAVES(K, DW), 8)))
-bits_step_kernel(BitsArgs a)
+template <int K, int DW>
+__global__ void __launch_bounds__(256) bits_step_kernel(BitsArgs a)
 {
     const int lane = threadIdx.x & 63;
     const int group = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -291,15 +211,15 @@ bits_step_kernel(BitsArgs a)
 
     // Row indices are wave-uniform 32-bit values (rows < 2^31), kept in SGPRs.
     const int R = (int)a.R;
-    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;                   // first output row
-    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));                // end output row
-    const int first_in = s0 - K;                                             // first input row
-    const int last_in = s1 + K - 1;                                          // last input row
+    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;  // first output row
+    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows)); // end output row
+    const int first_in = s0 - K;                              // first input row
+    const int last_in = s1 + K - 1;                           // last input row
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
 
-    // Input row y lives at base(y) + y*pitch with base = top + k*pitch (y < 0),
-    // mid (0 <= y < R) or bot - R*pitch (y >= R): a scalar row pointer plus a
-    // 32-bit per-lane byte offset (global_load ... saddr form).
+    // Input row y lives at base(y) + y*pitch with base = top + k*pitch (y < 0), mid
+    // (0 <= y < R) or bot - R*pitch (y >= R): a scalar row pointer plus a 32-bit per-lane
+    // byte offset (global_load ... saddr form).
     const uint32_t *top_adj = a.top + K * a.pitch;
     const uint32_t *bot_adj = a.bot - a.R * a.pitch;
     const uint32_t lane_off = (uint32_t)col * 4u;  // bytes
@@ -310,9 +230,8 @@ bits_step_kernel(BitsArgs a)
         return reinterpret_cast<const uint32_t *>(rb + lane_off);
     };
 
-    typedef PipeSel<K, DW, ALGO> PS;
-    typename PS::type p;
-    PS::init(p);
+    Pipe<K, DW> p;
+    pipe_init(p);
 
     uint32_t buf[3][DW];
 #pragma unroll
@@ -325,10 +244,9 @@ bits_step_kernel(BitsArgs a)
 #pragma unroll
         for (int s = 0; s < 3; ++s) load_words<DW>(row_ptr(first_in + t0 + 3 + s), nxt[s]);
 
-        // The three rows of this block run through the K stages as a wavefront
-        // (row S is at stage w - S), so every instruction has two independent
-        // neighbours to issue beside it and the DPP read-after-write hazards are
-        // covered without s_nop.
+        // The three rows of this block run through the K stages as a wavefront (row S is
+        // at stage w - S), so every instruction has two independent neighbours to issue
+        // beside it and the DPP read-after-write hazards are covered without s_nop.
         uint32_t cur[3][DW];
 #pragma unroll
         for (int s = 0; s < 3; ++s)
@@ -336,9 +254,9 @@ bits_step_kernel(BitsArgs a)
             for (int j = 0; j < DW; ++j) cur[s][j] = buf[s][j];
 #pragma unroll
         for (int w = 0; w < K + 2; ++w) {
-            if (w < K) PS::template stage<0>(p, w, cur[0]);
-            if (w >= 1 && w - 1 < K) PS::template stage<1>(p, w - 1, cur[1]);
-            if (w >= 2 && w - 2 < K) PS::template stage<2>(p, w - 2, cur[2]);
+            if (w < K) sstage<K, DW, 0>(p, w, cur[0]);
+            if (w >= 1 && w - 1 < K) sstage<K, DW, 1>(p, w - 1, cur[1]);
+            if (w >= 2 && w - 2 < K) sstage<K, DW, 2>(p, w - 2, cur[2]);
         }
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
@@ -346,12 +264,9 @@ bits_step_kernel(BitsArgs a)
             const int t = t0 + S;
             const int y = s0 + t - 2 * K;  // row emitted by the last stage
             if (t >= 2 * K && y < s1) {
-                if constexpr (ALGO == 1) {  // undo the K-bit frame shift
-                    const uint32_t nx0 = from_upper_lane(out[0]);
+                const uint32_t nx0 = from_upper_lane(out[0]);  // undo the K-bit frame shift
 #pragma unroll
-                    for (int j = 0; j < DW; ++j)
-                        out[j] = __builtin_amdgcn_alignbit(j == DW - 1 ? nx0 : out[j + 1], out[j], K);
-                }
+                for (int j = 0; j < DW; ++j) out[j] = __builtin_amdgcn_alignbit(j == DW - 1 ? nx0 : out[j + 1], out[j], K);
                 if (writer) {
                     char *rb = reinterpret_cast<char *>(a.dst + (int64_t)y * a.pitch);
                     store_words<DW>(reinterpret_cast<uint32_t *>(rb + lane_off), out);
@@ -370,24 +285,15 @@ bits_step_kernel(BitsArgs a)
     if (a.slots) slot_add(a.slots, alive);
 }
 
-// Store DW words at byte offset voff of a buffer [row, row + nbytes): out-of-range
-// offsets (and nbytes = 0) are dropped by the hardware range check.
+// Store DW words at byte offset voff of a buffer [row, row + nbytes): out-of-range offsets
+// (and nbytes = 0) are dropped by the hardware range check.  aux 2 = nt (streaming) stores.
 template <int DW>
-#ifndef GOL_ST_AUX
-#define GOL_ST_AUX 2  // nt (streaming) stores: +1 % measured; cache-policy bits of the band kernels' row stores (measurement knob)
-#endif
-#ifndef GOL_XCD_REMAP
-#define GOL_XCD_REMAP 1  // pipe kernel: contiguous runs of column groups per XCD
-#endif
-#ifndef GOL_LD_AUX
-#define GOL_LD_AUX 0  // cache-policy bits of the pipe kernel's global_load_lds (measurement knob)
-#endif
 __device__ __forceinline__ void store_row_masked(char *row, uint32_t nbytes, uint32_t voff, const uint32_t (&w)[DW])
 {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, (int)nbytes, 0x00020000);
     if constexpr (DW == 4) {
         typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, r, voff, 0, GOL_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, r, voff, 0, 2);
     } else if constexpr (DW == 2) {
         typedef __attribute__((ext_vector_type(2))) uint32_t v2u;
         __builtin_amdgcn_raw_buffer_store_b64(v2u{w[0], w[1]}, r, voff, 0, 0);
@@ -397,16 +303,15 @@ __device__ __forceinline__ void store_row_masked(char *row, uint32_t nbytes, uin
 }
 
 // ------------------------------------------------------------------ band-layout bit board
-// Column-band layout: a row is Wd = W/32 words and bit b of word w is cell
-// x = b*Wd + w (32 bands of Wd columns, one per bit).  The horizontal neighbours
-// of a cell are the SAME bit of the neighbouring words, so a generation is pure
-// bitwise logic: no v_alignbit (which issues at half the rate of v_bitop3 on
-// gfx950) and the centre cell is the word itself.  The column
-// torus wraps band b's last column onto band b+1's first: band-space column
-// c = q*Wd + r reads word r rotated right by q (one v_alignbit per word per
-// LOAD, only in the waves that straddle the wrap).  Cost: the horizontal halo
-// is now k words (k columns) instead of one 32-cell word, so a wave of 64 lanes
-// x 4 words keeps 64 - 2*ceil(k/4) lanes of output.
+// Column-band layout: a row is Wd = W/32 words and bit b of word w is cell x = b*Wd + w (32
+// bands of Wd columns, one per bit).  The horizontal neighbours of a cell are the SAME bit
+// of the neighbouring words, so a generation is pure bitwise logic: no v_alignbit (which
+// issues at half the rate of v_bitop3 on gfx950) and the centre cell is the
+// word itself.  The column torus wraps band b's last column onto band b+1's first:
+// band-space column c = q*Wd + r reads word r rotated right by q (one v_alignbit per word
+// per LOAD, only in the waves that straddle the wrap).  Cost: the horizontal halo is k words
+// (k columns) instead of one 32-cell word, so a wave of 64 lanes x DW words keeps
+// 64 - 2*ceil(k/DW) lanes of output.
 template <int DW>
 __device__ __forceinline__ void hsum_band(const uint32_t (&c)[DW], uint32_t (&h0)[DW], uint32_t (&h1)[DW])
 {
@@ -421,9 +326,9 @@ __device__ __forceinline__ void hsum_band(const uint32_t (&c)[DW], uint32_t (&h0
     }
 }
 
-// The rule is written op by op across the DW words (each op has DW-1 independent
-// neighbours): per word the 8 ops form a dependent chain, and a wave issues a dependent
-// VALU op ~1.7x slower than an independent one (MI355X_MICROARCH.md, constants table).
+// The rule written op by op across the DW words (each op has DW-1 independent neighbours):
+// per word the 8 ops form a dependent chain, and one wave issues a dependent VALU op ~1.7x
+// slower than an independent one (MI355X_MICROARCH.md, constants table).
 template <int K, int DW, int S>
 __device__ __forceinline__ void bstage(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
 {
@@ -453,7 +358,8 @@ __device__ __forceinline__ void bstage(Pipe<K, DW> &p, const int g, uint32_t (&c
     for (int j = 0; j < DW; ++j) cur[j] = bitop3<TT_MUX>(t0[j], e1[j], e2[j]);
 }
 
-// Same stage with the rule evaluated word by word (fewer live temporaries than bstage).
+// Same stage with the rule evaluated word by word (fewer live temporaries than bstage; at
+// 4 waves per SIMD a dependent op issues as fast as an independent one).
 template <int K, int DW, int S>
 __device__ __forceinline__ void bstage_seq(Pipe<K, DW> &p, const int g, uint32_t (&cur)[DW])
 {
@@ -467,61 +373,16 @@ __device__ __forceinline__ void bstage_seq(Pipe<K, DW> &p, const int g, uint32_t
                       p.h1[g][S][j], p.cc[g][SM][j]);
 }
 
-// Vertical-first stage (band layout): per word the vertical 3-sum of the column
-// (v0, v1) = c(y-1) + c(y) + c(y+1), then the horizontal sum of the three neighbouring
-// columns' (v0, v1) and the rule with the centre cell c(y).  Same 10 bitwise ops per word
-// as bstage (the sharing moves from vertical to horizontal: 2 DPP per lane edge instead
-// of 1), but the stage state is only the last two input rows: 2 VGPRs per word instead
-// of 5 (in the standard layout the same reordering doubled the shifts; here there are none).
-template <int K, int DW>
-struct PipeV {
-    uint32_t c[K][3][DW];
-};
-
-template <int K, int DW, int S>
-__device__ __forceinline__ void vstage(PipeV<K, DW> &p, const int g, uint32_t (&cur)[DW])
-{
-    constexpr int SA = (S + 1) % 3, SM = (S + 2) % 3;
-    uint32_t v0[DW], v1[DW];
-#pragma unroll
-    for (int j = 0; j < DW; ++j) {
-        p.c[g][S][j] = cur[j];
-        v0[j] = bitop3<TT_XOR3>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
-        v1[j] = bitop3<TT_MAJ>(p.c[g][SA][j], p.c[g][SM][j], cur[j]);
-    }
-    const uint32_t l0 = from_lower_lane(v0[DW - 1]), l1 = from_lower_lane(v1[DW - 1]);
-    const uint32_t r0 = from_upper_lane(v0[0]), r1 = from_upper_lane(v1[0]);
-#pragma unroll
-    for (int j = 0; j < DW; ++j) {
-        const uint32_t a0 = j == 0 ? l0 : v0[j - 1], a1 = j == 0 ? l1 : v1[j - 1];
-        const uint32_t c0 = j == DW - 1 ? r0 : v0[j + 1], c1 = j == DW - 1 ? r1 : v1[j + 1];
-        cur[j] = rule(a0, a1, v0[j], v1[j], c0, c1, p.c[g][SM][j]);
-    }
-}
-
 __host__ __device__ constexpr int band_halo_lanes(int k, int dw) { return (k + dw - 1) / dw; }
 __host__ __device__ constexpr int band_useful_words(int k, int dw) { return (64 - 2 * band_halo_lanes(k, dw)) * dw; }
 
-#ifndef GOL_SPLIT_KW
-#define GOL_SPLIT_KW 3  // stages per wave of the split pipeline
-#endif
-#ifndef GOL_SPLIT_MIN_WAVES
-#define GOL_SPLIT_MIN_WAVES 4
-#endif
-#ifndef GOL_BAND_PREFETCH
-#define GOL_BAND_PREFETCH 1  // row blocks loaded ahead of use
-#endif
-#ifndef GOL_BAND_MIN_WAVES
-#define GOL_BAND_MIN_WAVES 1
-#endif
-
-// Same row addressing, strips and fused count as bits_step_kernel; grid.x: groups
-// of 4 waves along the row, grid.y: strips of output rows.  A lane holds DW words.
+// One wave = all K stages (k = 1, 2, 4, 8; 16 with 2 words per lane).  Same row addressing,
+// strips and fused count as bits_step_kernel; grid.x: groups of 4 waves along the row,
+// grid.y: strips of output rows.
 // CONTIG: top == mid - K*pitch and bot == mid + R*pitch (halo rows stored right above and
 // below the shard), so input row y is simply mid + y*pitch: no per-row segment select.
-template <int K, int DW, bool CONTIG, bool VF = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GOL_BAND_MIN_WAVES, 8)))
-band_step_kernel(BitsArgs a)
+template <int K, int DW, bool CONTIG>
+__global__ void __launch_bounds__(256) band_step_kernel(BitsArgs a)
 {
     constexpr int HL = band_halo_lanes(K, DW);
     constexpr int U = band_useful_words(K, DW);
@@ -541,25 +402,24 @@ band_step_kernel(BitsArgs a)
     const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
     const int first_in = s0 - K;
     const int last_in = s1 + K - 1;
-    constexpr int NB = GOL_BAND_PREFETCH + 1;  // blocks per loop trip (see the ring below)
+    constexpr int NB = 2;  // blocks per loop trip: the ring below (one block loaded ahead)
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
     const int nblk_r = (nblk + NB - 1) / NB * NB;  // trailing blocks re-read the last row, store nothing
 
-    // Scalar row base + 32-bit products (the row pitch in bytes fits 32 bits: W < 2^34 cells).
     // Every row address is a.mid + (segment displacement + y * pitch): one pointer (the
-    // compiler keeps it in the global address space, so the loads are global_load with
-    // exact vmcnt waits) plus an integer select.  A select between pointer locals can
-    // become an indexed private array (scratch loads in the loop); an integer-to-pointer
-    // cast becomes a flat load (vmcnt(0) + lgkmcnt waits).
+    // compiler keeps it in the global address space, so the loads are global_load with exact
+    // vmcnt waits) plus an integer select.  A select between pointer locals can become an
+    // indexed private array (scratch loads in the loop); an integer-to-pointer cast becomes a
+    // flat load (vmcnt(0) + lgkmcnt waits).
     const int pitch_b = (int)a.pitch * 4;
     const char *mid_b = reinterpret_cast<const char *>(a.mid);
     const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch_b;
     const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch_b;
     const uint32_t lane_off = (uint32_t)col * 4u;
     // Stores: buffer stores with the row as the buffer range, so rows that must not be
-    // written (pipeline fill, past the strip) and halo lanes are dropped by the range
-    // check instead of a branch (stores under a branch make the compiler's vmcnt waits
-    // for the NEXT block's rows also wait for these stores).
+    // written (pipeline fill, past the strip) and halo lanes are dropped by the range check
+    // instead of a branch (stores under a branch make the compiler's vmcnt waits for the NEXT
+    // block's rows also wait for these stores).
     char *dst_b = reinterpret_cast<char *>(a.dst);
     const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
@@ -577,32 +437,20 @@ band_step_kernel(BitsArgs a)
         }
     };
 
-    typename std::conditional<VF, PipeV<K, DW>, Pipe<K, DW>>::type p;
-    if constexpr (VF) {
-#pragma unroll
-        for (int g = 0; g < K; ++g)
-#pragma unroll
-            for (int s2 = 0; s2 < 3; ++s2)
-#pragma unroll
-                for (int j = 0; j < DW; ++j) p.c[g][s2][j] = 0;
-    } else {
-        PipeSel<K, DW, 0>::init(p);
-    }
+    Pipe<K, DW> p;
+    pipe_init(p);
 
-    // Row blocks in flight: a ring of PF+1 three-row buffers; block b lives in ring[b % (PF+1)]
-    // and is loaded PF blocks ahead of use.  The block loop is unrolled by PF+1 so the ring
-    // index is static: no register copies, and the loads are waited for just before their
-    // first use (a copy at the loop end would also wait for that block's stores: gfx9 has
-    // one in-order vmcnt for loads and stores).
-    constexpr int PF = GOL_BAND_PREFETCH;
+    // Row blocks in flight: a ring of NB three-row buffers; block b lives in ring[b % NB] and
+    // is loaded one block ahead of use.  The block loop is unrolled by NB so the ring index is
+    // static: no register copies, and the loads are waited for just before their first use (a
+    // copy at the loop end would also wait for that block's stores: gfx9 has one in-order
+    // vmcnt for loads and stores).
     uint32_t ring[NB][3][DW];
 #pragma unroll
-    for (int b = 0; b < PF; ++b)
-#pragma unroll
-        for (int s = 0; s < 3; ++s) load_row(first_in + 3 * b + s, ring[b][s]);
-    // Three empty-range stores (dropped) so that the loop is entered with the same
-    // memory-counter history as its back edge (loads, then a block's 3 stores): the
-    // compiler then waits for the block's rows with vmcnt(6), not vmcnt(3).
+    for (int s = 0; s < 3; ++s) load_row(first_in + s, ring[0][s]);
+    // Three empty-range stores (dropped) so that the loop is entered with the same memory-
+    // counter history as its back edge (loads, then a block's 3 stores): the compiler then
+    // waits for the block's rows with vmcnt(6), not vmcnt(3).
 #pragma unroll
     for (int s = 0; s < 3; ++s) store_row_masked<DW>(dst_b, 0u, st_off, ring[0][s]);
 
@@ -612,21 +460,15 @@ band_step_kernel(BitsArgs a)
         for (int u = 0; u < NB; ++u) {
             const int t0 = (blk0 + u) * 3;
 #pragma unroll
-            for (int s = 0; s < 3; ++s) load_row(first_in + t0 + 3 * PF + s, ring[(u + PF) % NB][s]);
+            for (int s = 0; s < 3; ++s) load_row(first_in + t0 + 3 + s, ring[(u + 1) % NB][s]);
             uint32_t (&cur)[3][DW] = ring[u];
 #pragma unroll
             for (int s = 0; s < 3; ++s) unwrap(cur[s]);
 #pragma unroll
             for (int w = 0; w < K + 2; ++w) {
-                if constexpr (VF) {
-                    if (w < K) vstage<K, DW, 0>(p, w, cur[0]);
-                    if (w >= 1 && w - 1 < K) vstage<K, DW, 1>(p, w - 1, cur[1]);
-                    if (w >= 2 && w - 2 < K) vstage<K, DW, 2>(p, w - 2, cur[2]);
-                } else {
-                    if (w < K) bstage<K, DW, 0>(p, w, cur[0]);
-                    if (w >= 1 && w - 1 < K) bstage<K, DW, 1>(p, w - 1, cur[1]);
-                    if (w >= 2 && w - 2 < K) bstage<K, DW, 2>(p, w - 2, cur[2]);
-                }
+                if (w < K) bstage<K, DW, 0>(p, w, cur[0]);
+                if (w >= 1 && w - 1 < K) bstage<K, DW, 1>(p, w - 1, cur[1]);
+                if (w >= 2 && w - 2 < K) bstage<K, DW, 2>(p, w - 2, cur[2]);
             }
 #pragma unroll
             for (int S = 0; S < 3; ++S) {
@@ -647,192 +489,10 @@ band_step_kernel(BitsArgs a)
     if (a.slots) slot_add(a.slots, alive);
 }
 
-// ------------------------------------------------------------------ band layout, split pipeline
-// The K stages of band_step_kernel split over P waves of one workgroup, KW = K/P stages
-// each: wave w runs stages [w*KW, (w+1)*KW) and hands every block of 3 rows to wave w+1
-// through LDS.  A wave then holds 5*KW*4 pipeline VGPRs instead of 5*K*4, which fits
-// 4 waves per SIMD: v_bitop3_b32 issues at ~1.9 SIMD cycles per wave64 instruction at 4
-// waves per SIMD against ~2.8 at 2 (tools/ubench/valu_dep.hip), and K = 12 keeps HBM
-// at ~1/12 of a board pass per turn.  Wave 0 stages the input rows HBM -> LDS with
-// global_load_lds (no VGPRs); every wave reads its input block with ds_read_b128.
-// Periods: in period j wave w works on block j - w; one workgroup barrier per period
-// (LDS slots are double-buffered by block parity).
-template <int DW>
-__device__ __forceinline__ void lds_read_row(const uint32_t *slot, int lane, uint32_t (&w)[DW])
-{
-    static_assert(DW == 4, "the split pipeline keeps 4 words per lane");
-    const uint4 v = reinterpret_cast<const uint4 *>(slot)[lane];
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-}
-template <int DW>
-__device__ __forceinline__ void lds_write_row(uint32_t *slot, int lane, const uint32_t (&w)[DW])
-{
-    reinterpret_cast<uint4 *>(slot)[lane] = make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-template <int KW, int P, bool CONTIG>
-__global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(GOL_SPLIT_MIN_WAVES, 8)))
-band_split_kernel(BitsArgs a)
-{
-    constexpr int DW = 4;
-    constexpr int K = KW * P;
-    constexpr int HL = band_halo_lanes(K, DW);
-    constexpr int U = band_useful_words(K, DW);
-    constexpr int ROW = 64 * DW;  // uint32 per LDS row slot (1 KiB)
-    // LDS: input slots of wave 0 (filled by global_load_lds; one array per block parity so
-    // the compiler sees that a staging DMA never aliases the slot being read) and the
-    // hand-off slots of waves 0 .. P-2, [parity][row of block][lane][DW words].
-    __shared__ uint32_t lds_in0[3][ROW], lds_in1[3][ROW];
-    __shared__ uint32_t lds_x[P - 1][2][3][ROW];
-
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // pipeline position
-    const int group = blockIdx.x;
-
-    const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
-    const int64_t q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
-    const int64_t col = col_raw - q * a.Wd;
-    const uint32_t rot = (uint32_t)q & 31u;
-    const bool wrap = __ballot(rot != 0) != 0;
-    const bool writer = lane >= HL && lane < 64 - HL && col_raw < a.Wd;
-
-    const int R = (int)a.R;
-    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
-    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
-    const int first_in = s0 - K;
-    const int last_in = s1 + K - 1;
-    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
-
-    const int pitch_b = (int)a.pitch * 4;
-    const char *mid_b = reinterpret_cast<const char *>(a.mid);
-    const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch_b;
-    const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch_b;
-    const uint32_t lane_off = (uint32_t)col * 4u;
-    char *dst_b = reinterpret_cast<char *>(a.dst);
-    const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
-    const uint32_t st_off = writer ? lane_off : 0x80000000u;
-
-    // wave 0: the 3 rows of block b -> slot (global_load_lds: lane l writes 16 B at l*16)
-    auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            int y = first_in + 3 * b + s;
-            y = y > last_in ? last_in : y;
-            const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
-            const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
-        }
-    };
-
-    Pipe<KW, DW> p;
-    PipeSel<KW, DW, 0>::init(p);
-    if (wv == 0) {
-        stage_in(0, lds_in0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-    uint32_t alive = 0;
-    // One period: this wave's block b = period - wv.  PAR = period parity (static, so wave
-    // 0's input slot and staging slot are distinct arrays).
-    auto period_body = [&](const int period, auto par) {
-        constexpr int PAR = decltype(par)::value;
-        const int b = period - wv;
-        if (b >= 0 && b < nblk) {
-            if (wv == 0 && b + 1 < nblk) stage_in(b + 1, PAR ? lds_in0 : lds_in1);  // slot freed last period
-            const uint32_t *src = wv == 0 ? &(PAR ? lds_in1 : lds_in0)[0][0] : &lds_x[wv == 0 ? 0 : wv - 1][b & 1][0][0];
-            uint32_t *dstx = &lds_x[wv < P - 1 ? wv : 0][b & 1][0][0];
-#pragma unroll
-            for (int S = 0; S < 3; ++S) {
-                uint32_t cur[DW];
-                lds_read_row<DW>(src + S * ROW, lane, cur);
-                if (wv == 0 && wrap) {
-#pragma unroll
-                    for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
-                }
-                // one row through this wave's KW stages (at 4 waves per SIMD a dependent VALU
-                // op issues as fast as an independent one: no wavefront interleave needed)
-#pragma unroll
-                for (int g = 0; g < KW; ++g) {
-                    if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
-                    if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
-                    if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
-                }
-                if (wv == P - 1) {
-                    const int t = 3 * b + S;
-                    const int y = s0 + t - 2 * K;
-                    const bool row_ok = t >= 2 * K && y < s1;
-                    store_row_masked<DW>(dst_b + (int64_t)(row_ok ? y : s0) * pitch_b, row_ok ? row_bytes : 0u,
-                                         st_off, cur);
-                    if (a.slots) {
-                        uint32_t c = 0;
-#pragma unroll
-                        for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
-                        alive += (row_ok && writer) ? c : 0u;
-                    }
-                } else {
-                    lds_write_row<DW>(dstx + S * ROW, lane, cur);
-                }
-            }
-        }
-        if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next block staged
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    const int nper = nblk + P - 1;
-    int period = 0;
-    for (; period + 1 < nper; period += 2) {
-        period_body(period, std::integral_constant<int, 0>());
-        period_body(period + 1, std::integral_constant<int, 1>());
-    }
-    if (period < nper) period_body(period, std::integral_constant<int, 0>());
-    if (a.slots && wv == P - 1) slot_add(a.slots, alive);
-}
-
-// Flag-synchronised split pipeline (no workgroup barriers): wave w consumes ring w (ring
-// 0 = the input rows, staged by wave 0 itself with global_load_lds) and produces ring
-// w+1; each ring has NS slots of one block (3 rows).  ready[e] = blocks published into
-// ring e, consumed[e] = blocks taken out of it.  A producer may fill slot b % NS once its
-// consumer has taken block b - NS; a consumer may read block b once ready > b.  The chain
-// has no cycle, and every spin is bounded (a protocol fault ends the wave, and the parity
-// tests then fail, instead of hanging the GPU).
-#ifndef GOL_BAND_VF_DEFAULT
-#define GOL_BAND_VF_DEFAULT 0  // 1: band k = 8/12/16 with 4 words per lane on the vertical-first kernel
-#endif
-#ifndef GOL_PIPE_VF_DEFAULT
-#define GOL_PIPE_VF_DEFAULT 0  // 1: k = 12 as GOL_PIPE_VF_P waves of vertical-first stages
-#endif
-#ifndef GOL_PIPE_VF_P
-#define GOL_PIPE_VF_P 2
-#endif
-#ifndef GOL_PIPE_ROTATE
-#define GOL_PIPE_ROTATE 1  // rotate pipeline roles over the SIMDs by workgroup
-#endif
-#ifndef GOL_PIPE_PROFILE
-#define GOL_PIPE_PROFILE 0  // diagnostic build: per-role wait-cycle sums instead of the alive count
-#endif
-#ifndef GOL_PIPE_ABL
-#define GOL_PIPE_ABL 0  // measurement only (wrong results): 1 = no flag waits, 2 = no LDS row traffic,
-                        // 4 = no HBM traffic, 8 = no stores, 16 = no input loads
-#endif
-#ifndef GOL_SPIN_SLEEP
-#define GOL_SPIN_SLEEP 1  // s_sleep argument between flag polls (units of 64 cycles)
-#endif
-#ifndef GOL_PIPE_IN_SLOTS
-#define GOL_PIPE_IN_SLOTS 3  // input ring slots (staging runs NSI-1 blocks ahead; 4 and 5 measured no faster)
-#endif
-#ifndef GOL_PIPE_SLOTS
-#define GOL_PIPE_SLOTS 3
-#endif
-#ifndef GOL_PIPE_PRIO
-#define GOL_PIPE_PRIO 0  // wave priority by role: 0 = equal, 1 = upstream first, 2 = downstream first
-#endif
-#ifndef GOL_PIPE_LGKM
-#define GOL_PIPE_LGKM 2  // 2: per-role loops unrolled over the ring slots; 1: per-role loops; 0: first loop
-#endif
-// LDS accesses of the pipeline are inline asm: the compiler treats a global_load_lds in
+// ------------------------------------------------------------------ LDS helpers of the pipelines
+// LDS accesses of the pipelines are inline asm: the compiler treats a global_load_lds in
 // flight as a pending LDS write and would put vmcnt(0) before every LDS access it can see
-// (which, on the storing wave, also waits for its HBM stores).  Each read waits for its own
-// result (lgkmcnt(0)); the LDS latency is hidden by the other waves of the SIMD.
+// (which, on the storing wave, also waits for its HBM stores).
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u32;
 __device__ __forceinline__ v4u32 lds_rd128(const lds_u32 *p)
@@ -841,18 +501,10 @@ __device__ __forceinline__ v4u32 lds_rd128(const lds_u32 *p)
     asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(p) : "memory");
     return r;
 }
-// Split issue / wait: the wait takes the value as an in-out operand, so every use of it is
-// ordered after the wait.
-__device__ __forceinline__ v4u32 lds_rd128_issue(const lds_u32 *p)
-{
-    v4u32 r;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(p) : "memory");
-    return r;
-}
-__device__ __forceinline__ void lds_wait(v4u32 &r) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r)::"memory"); }
 // Wait for a read with N younger LDS operations allowed in flight (LDS operations of a wave
 // complete in order, and these kernels issue no scalar loads in the loop; the assembly check
-// tools/check_lds_wait.py confirms the latter).
+// tools/check_lds_wait.py confirms the latter).  The value is an in-out operand, so every
+// use of it is ordered after the wait.
 template <int N>
 __device__ __forceinline__ void lds_wait_n(v4u32 &r)
 {
@@ -877,10 +529,6 @@ __device__ __forceinline__ void lds_wr128_o(lds_u32 *p, v4u32 v)
 // Flag write without an exec mask: lane 0's address is the flag, the other lanes write their
 // own scratch word (one ds_write, no saveexec / branch around it).
 __device__ __forceinline__ void lds_flag_wr(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
-__device__ __forceinline__ void lds_wr128(lds_u32 *p, v4u32 v)
-{
-    asm volatile("ds_write_b128 %0, %1" ::"v"(p), "v"(v) : "memory");
-}
 __device__ __forceinline__ int lds_rd32(const lds_u32 *p)
 {
     int r;
@@ -889,21 +537,33 @@ __device__ __forceinline__ int lds_rd32(const lds_u32 *p)
 }
 __device__ __forceinline__ void lds_wr32(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
 // Wait until flag f >= v; returns the value seen (callers cache it: a producer is usually
-// several blocks ahead, so most blocks need no flag read), or -1 after the spin bound.
+// several blocks ahead, so most blocks need no flag read), or -1 after GOL_SPIN_LIMIT polls.
+// A wave that sees -1 leaves its loop, every wave waiting on it times out the same way, and
+// each records GOLK_ERR_SPIN in the launch's error word on its way out (once, after the loop:
+// an atomic inside the loop costs the pipeline registers), so the host reports the launch as
+// failed (GOL_EHIP) instead of returning a board with unwritten strips.
 __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 {
 #pragma clang loop unroll(disable)
-    for (int n = 0; n < (1 << 22); ++n) {
+    for (int n = 0; n < GOL_SPIN_LIMIT; ++n) {
         const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
         if (x >= v) return x;
-        __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
+        __builtin_amdgcn_s_sleep(1);
     }
     return -1;
 }
 
-template <int KW, int P, bool CONTIG, bool VF = false>
+// ------------------------------------------------------------------ band layout, split pipeline
+// The K = KW*P stages split over the P waves of one workgroup: wave w runs stages
+// [w*KW, (w+1)*KW) and hands every block of 3 rows to wave w+1 through an LDS ring (3 slots
+// of one block).  A wave then holds 5*KW*4 pipeline VGPRs instead of 5*K*4, which fits 4
+// waves per SIMD.  Wave 0 stages its input rows HBM -> LDS with global_load_lds (no VGPRs),
+// wave P-1 stores to HBM.  Synchronisation is per ring, by LDS flags: ready[e] = blocks
+// published into ring e, consumed[e] = blocks taken out of it; a producer fills slot b % 3
+// once block b-3 is consumed.  Every spin is bounded (spin_until_ge).
+template <int KW, int P, bool CONTIG>
 __global__ void __launch_bounds__(64 * P)
-__attribute__((amdgpu_waves_per_eu(KW >= 4 && !VF ? 3 : GOL_SPLIT_MIN_WAVES, 8)))  // 5 KW DW pipeline VGPRs
+__attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
 band_pipe_kernel(BitsArgs a)
 {
     constexpr int DW = 4;
@@ -911,23 +571,18 @@ band_pipe_kernel(BitsArgs a)
     constexpr int HL = band_halo_lanes(K, DW);
     constexpr int U = band_useful_words(K, DW);
     constexpr int ROW = 64 * DW;
-    constexpr int NS = GOL_PIPE_SLOTS;
-    constexpr int NSI = GOL_PIPE_IN_SLOTS;  // input ring: blocks b .. b+NSI-2 in flight
-    __shared__ uint32_t in_ring[NSI][3][ROW];
+    constexpr int NS = 3;
+    __shared__ uint32_t in_ring[NS][3][ROW];
     __shared__ uint32_t ring[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
     __shared__ int ready[P], consumed[P];
-    __shared__ int flag_scratch[GOL_PIPE_LGKM == 2 ? P : 1][64];
-    (void)flag_scratch;
+    __shared__ int flag_scratch[P][64];
 
     const int lane = threadIdx.x & 63;
-    // Pipeline position of this wave.  Rotated by workgroup: the waves of a workgroup sit on
-    // the CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put
-    // its loader (global_load_lds) on one SIMD and its storer on another.
     // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (L2 per XCD), so
     // consecutive ids are remapped to let each XCD walk its own contiguous run of column groups
     // of a strip: the lateral halo columns two neighbouring groups both read then meet in one L2.
     int bx = blockIdx.x, by = blockIdx.y;
-    if (GOL_XCD_REMAP) {
+    {
         const int n = gridDim.x * gridDim.y, l = blockIdx.x + blockIdx.y * gridDim.x;
         const int per = n / 8;
         if (l < per * 8) {
@@ -936,7 +591,10 @@ band_pipe_kernel(BitsArgs a)
             by = m / gridDim.x;
         }
     }
-    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + GOL_PIPE_ROTATE * (bx + by)) % P);
+    // Pipeline position of this wave, rotated by workgroup: the waves of a workgroup sit on
+    // the CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put
+    // its loader (global_load_lds) on one SIMD and its storer on another.
+    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + (bx + by)) % P);
     const int group = bx;
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
@@ -959,11 +617,9 @@ band_pipe_kernel(BitsArgs a)
     const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch_b;
     const uint32_t lane_off = (uint32_t)col * 4u;
     char *dst_b = reinterpret_cast<char *>(a.dst);
-    const uint32_t row_bytes = (uint32_t)a.Wd * 4u;
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
-    (void)row_bytes;
 
-    // wave 0: block b -> in_ring[b % NSI] (global_load_lds).  The slot is an argument: a lambda
+    // wave 0: block b -> in_ring[b % NS] (global_load_lds).  The slot is an argument: a lambda
     // that captures a __shared__ array silently loses the kernel's host-side stub.
     auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
 #pragma unroll
@@ -972,7 +628,7 @@ band_pipe_kernel(BitsArgs a)
             y = y > last_in ? last_in : y;
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, GOL_LD_AUX);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
         }
     };
 
@@ -983,50 +639,18 @@ band_pipe_kernel(BitsArgs a)
     lds_u32 *const ready_l = (lds_u32 *)&ready[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
     constexpr int SLOT = 3 * ROW;  // uint32 per slot (one block)
-    auto slot_row = [&](int e, int b, int S) {
-        return e == 0 ? in_l + (b % NSI) * SLOT + S * ROW + lane * 4
-                      : ring_l + ((e - 1) * NS + b % NS) * SLOT + S * ROW + lane * 4;
-    };
 
-    typename std::conditional<VF, PipeV<KW, DW>, Pipe<KW, DW>>::type p;
-    if constexpr (VF) {
-#pragma unroll
-        for (int g = 0; g < KW; ++g)
-#pragma unroll
-            for (int s2 = 0; s2 < 3; ++s2)
-#pragma unroll
-                for (int j = 0; j < DW; ++j) p.c[g][s2][j] = 0;
-    } else {
-        PipeSel<KW, DW, 0>::init(p);
-    }
-    if (wv == 0) {
-#pragma unroll
-        for (int i = 0; i < NSI - 1; ++i)
-            if (i < nblk) stage_in(i, in_ring[i]);
-    }
+    Pipe<KW, DW> p;
+    pipe_init(p);
     uint32_t alive = 0;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
-    bool ok = true;
-    v4u32 fake = v4u32{(uint32_t)lane, 7u, (uint32_t)blockIdx.x, 9u};  // GOL_PIPE_ABL & 2 only
     int seen_ready = 0, seen_free = 0;  // cached flag values (ring wv ready, ring wv+1 consumed)
-    // last wave: row y = s0 + 3b + S - 2K is stored iff 0 <= 3b + S - 2K < s1 - s0
     const uint32_t nrows = (uint32_t)(s1 - s0);
-    char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch_b;  // row of (b, S) = (0, 0), advanced per row
-#if GOL_PIPE_PROFILE
-    uint64_t pt_in = 0, pt_free = 0, pt_lds = 0, pt_mark;
-    const uint64_t pt0 = __builtin_amdgcn_s_memtime();
-#define PT_BEGIN() pt_mark = __builtin_amdgcn_s_memtime()
-#define PT_END(acc) acc += __builtin_amdgcn_s_memtime() - pt_mark
-#else
-#define PT_BEGIN()
-#define PT_END(acc)
-#endif
-#if GOL_PIPE_LGKM == 2
     // One loop per role (0 = loader, 1 = middle, 2 = last), unrolled over the 3 ring slots so
     // every LDS address is a per-lane register plus an immediate offset and every wait count is
-    // a constant.  The loop carries no other per-block arithmetic than the flag values:
-    // the per-block instruction count is what bounds this kernel (all waves issue through the
-    // same per-SIMD slots, so scalar and branch instructions cost about as much as VALU ones).
+    // a constant.  The loop carries no other per-block arithmetic than the flag values: the
+    // per-block instruction count is what bounds this kernel (all waves issue through the same
+    // per-SIMD slots, so scalar and branch instructions cost about as much as VALU ones).
     //  * row S+1 is read while row S computes; a row wait leaves the youngest LDS operation
     //    (this wave's previous ds_write or flag write) in flight: lgkmcnt(1);
     //  * the reading waves issue row 0 of block b+1 at row 2 of block b (spinning there if its
@@ -1035,23 +659,18 @@ band_pipe_kernel(BitsArgs a)
     //    writes of block b-1 are done (lgkmcnt(1) leaves only the row-1 read in flight);
     //  * the block count is padded to a multiple of 3: padding blocks read clamped rows and
     //    their stores fall outside the strip's buffer range.
-    static_assert(NS == 3 && NSI == 3, "the unrolled loop assumes 3-slot rings");
-    (void)ok; (void)fake; (void)slot_row; (void)srow; (void)st_mask;
     const int nblk3 = (nblk + 2) / 3 * 3;
     constexpr int SB = SLOT * 4, RB = ROW * 4;  // slot and row strides in bytes
-    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0][0] + (GOL_PIPE_LGKM == 2 ? wv : 0) * 64 + lane;
-    lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;      // writer: ring wv+1 ready
-    lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;       // reader: ring wv consumed
+    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0][0] + wv * 64 + lane;
+    lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // writer: ring wv+1 ready
+    lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // reader: ring wv consumed
     lds_u32 *const in_base = in_l + lane * 4;
     lds_u32 *const rd_base = ring_l + (wv - 1) * NS * SLOT + lane * 4;  // ring wv (wv >= 1)
     lds_u32 *const wr_base = ring_l + wv * NS * SLOT + lane * 4;        // ring wv+1 (wv < P-1)
     auto compute = [&](auto s_c, uint32_t (&cur)[DW]) {
         constexpr int S = decltype(s_c)::value;
 #pragma unroll
-        for (int g = 0; g < KW; ++g) {
-            if constexpr (VF) vstage<KW, DW, S>(p, g, cur);
-            else bstage_seq<KW, DW, S>(p, g, cur);
-        }
+        for (int g = 0; g < KW; ++g) bstage_seq<KW, DW, S>(p, g, cur);
     };
     auto unpack = [&](const v4u32 v, uint32_t (&cur)[DW]) { cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w; };
     auto pack = [&](const uint32_t (&cur)[DW]) { return v4u32{cur[0], cur[1], cur[2], cur[3]}; };
@@ -1071,13 +690,11 @@ band_pipe_kernel(BitsArgs a)
     const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
         dst_b + (int64_t)s0 * pitch_b, (short)0, (int)(nrows * (uint32_t)pitch_b), 0x00020000);
     uint32_t voff = st_off - (uint32_t)(2 * K) * (uint32_t)pitch_b;
-    const uint32_t strip_bytes = nrows * (uint32_t)pitch_b;
     int rrel = -2 * K;  // output row - s0 (wave-uniform)
     auto emit = [&](const uint32_t (&cur)[DW]) {
-        typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{cur[0], cur[1], cur[2], cur[3]}, strip_rs, voff, 0, GOL_ST_AUX);
-        // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are
-        // masked once at the end)
+        __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, 2);
+        // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are masked
+        // once at the end)
         if (a.slots && (uint32_t)rrel < nrows)
             alive += __popc(cur[0]) + __popc(cur[1]) + __popc(cur[2]) + __popc(cur[3]);
         voff += (uint32_t)pitch_b;
@@ -1092,13 +709,15 @@ band_pipe_kernel(BitsArgs a)
         asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     } else if (seen_ready < 1) {
         seen_ready = spin_until_ge(ready_l + wv, 1);
-        if (seen_ready < 0) return;
+        if (seen_ready < 0) {
+            raise_error(a.err, GOLK_ERR_SPIN);
+            return;
+        }
     }
     v4u32 nextv = lds_rd128(src_base);
     lds_flag_wr(wv == 0 ? scratch : cns_addr, 0);  // one younger LDS operation for block 0's wait
-    // ROLE 0 = loader (input from in_ring, staged from HBM), 1 = middle, 2 = last (stores)
     auto step = [&](int b, auto u_c, auto role_c) -> bool {
-        constexpr int U = decltype(u_c)::value;
+        constexpr int US = decltype(u_c)::value;
         constexpr int ROLE = decltype(role_c)::value;
         constexpr bool LAST = ROLE == 2;
         uint32_t cur[DW];
@@ -1111,30 +730,30 @@ band_pipe_kernel(BitsArgs a)
         // row 0
         lds_wait_n<1>(nextv);  // younger: the consumed flag / scratch write, the previous row-2 write
         unpack(nextv, cur);
-        nextv = lds_rd128_issue_o<U * SB + RB>(src_base);
+        nextv = lds_rd128_issue_o<US * SB + RB>(src_base);
         realign();
         compute(std::integral_constant<int, 0>(), cur);
         if constexpr (LAST) {
             emit(cur);
         } else {
             if (!publish_and_reserve(b)) return false;
-            lds_wr128_o<U * SB>(wr_base, pack(cur));
+            lds_wr128_o<US * SB>(wr_base, pack(cur));
         }
         // row 1
         lds_wait_n<LAST ? 0 : 1>(nextv);
         unpack(nextv, cur);
-        nextv = lds_rd128_issue_o<U * SB + 2 * RB>(src_base);
+        nextv = lds_rd128_issue_o<US * SB + 2 * RB>(src_base);
         realign();
         compute(std::integral_constant<int, 1>(), cur);
         if constexpr (LAST) emit(cur);
-        else lds_wr128_o<U * SB + RB>(wr_base, pack(cur));
+        else lds_wr128_o<US * SB + RB>(wr_base, pack(cur));
         // row 2; row 0 of block b+1 is read during it
         lds_wait_n<LAST ? 0 : 1>(nextv);
         unpack(nextv, cur);
         if constexpr (ROLE == 0) {
-            stage_in(b + 2, in_ring[(U + 2) % 3]);               // refills block b-1's slot (clamped past the end)
-            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");     // block b+1 landed, b+2 in flight
-            nextv = lds_rd128_issue_o<((U + 1) % 3) * SB>(src_base);
+            stage_in(b + 2, in_ring[(US + 2) % 3]);           // refills block b-1's slot (clamped past the end)
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // block b+1 landed, b+2 in flight
+            nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
             lds_flag_wr(scratch, 0);
         } else {
             if (b + 1 < nblk3) {
@@ -1142,248 +761,35 @@ band_pipe_kernel(BitsArgs a)
                     seen_ready = spin_until_ge(ready_l + wv, b + 2);
                     if (seen_ready < 0) return false;
                 }
-                nextv = lds_rd128_issue_o<((U + 1) % 3) * SB>(src_base);
+                nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
             }
             lds_flag_wr(cns_addr, b + 1);
         }
         realign();
         compute(std::integral_constant<int, 2>(), cur);
         if constexpr (LAST) emit(cur);
-        else lds_wr128_o<U * SB + 2 * RB>(wr_base, pack(cur));
+        else lds_wr128_o<US * SB + 2 * RB>(wr_base, pack(cur));
         return true;
     };
-    auto run = [&](auto role_c) {
+    auto run = [&](auto role_c) -> bool {
         for (int b = 0; b < nblk3; b += 3) {
-            if (!step(b, std::integral_constant<int, 0>(), role_c)) return;
-            if (!step(b + 1, std::integral_constant<int, 1>(), role_c)) return;
-            if (!step(b + 2, std::integral_constant<int, 2>(), role_c)) return;
+            if (!step(b, std::integral_constant<int, 0>(), role_c)) return false;
+            if (!step(b + 1, std::integral_constant<int, 1>(), role_c)) return false;
+            if (!step(b + 2, std::integral_constant<int, 2>(), role_c)) return false;
         }
         if constexpr (decltype(role_c)::value != 2) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_flag_wr(rdy_addr, nblk3);
         }
+        return true;
     };
-    if (wv == 0) run(std::integral_constant<int, 0>());
-    else if (wv == P - 1) run(std::integral_constant<int, 2>());
-    else run(std::integral_constant<int, 1>());
+    bool ok;
+    if (wv == 0) ok = run(std::integral_constant<int, 0>());
+    else if (wv == P - 1) ok = run(std::integral_constant<int, 2>());
+    else ok = run(std::integral_constant<int, 1>());
+    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
     alive &= st_mask;  // halo lanes' rows are not this group's
-    (void)strip_bytes;
-#elif GOL_PIPE_LGKM
-    // One loop per role (0 = loader, 1 = middle, 2 = storer), so every LDS wait has a count
-    // known at compile time.  Row S+1 is read while row S computes; a row wait lets the one
-    // younger LDS operation (the previous row's ds_write) stay in flight instead of draining
-    // it (lgkmcnt(1)); the middle and last waves read row 0 of the next block during row 2
-    // when its flag is already known to be set; "block b-1 ready" is published after row 0
-    // of block b, by when block b-1's writes have completed.
-    auto role_loop = [&](auto role_c) {
-        constexpr int ROLE = decltype(role_c)::value;
-        constexpr bool WRITES = ROLE != 2;  // writes the next wave's ring
-        constexpr int ABL = GOL_PIPE_ABL;    // measurement-only ablations (wrong results)
-        if constexpr (GOL_PIPE_PRIO == 1) __builtin_amdgcn_s_setprio(ROLE == 0 ? 3 : (ROLE == 1 ? 2 : 0));
-        if constexpr (GOL_PIPE_PRIO == 2) __builtin_amdgcn_s_setprio(ROLE == 2 ? 3 : (ROLE == 1 ? 1 : 0));
-        v4u32 nextv = fake;
-        bool pre = false;  // row 0 of block b already issued into nextv
-        for (int b = 0; b < nblk; ++b) {
-#pragma unroll
-            for (int S = 0; S < 3; ++S) {
-                uint32_t cur[DW];
-                v4u32 v;
-                if (S == 0) {
-                    PT_BEGIN();
-                    if (ROLE == 0 && !(ABL & 4)) {
-                        // block b landed; blocks b+1 .. b+NSI-2 (if any) may stay in flight
-                        const int inflight = min(NSI - 2, nblk - 1 - b);
-                        if (inflight >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-                        else if (inflight == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                        else if (inflight == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    }
-                    if (ABL & 2) {
-                        v = fake;
-                    } else if (ROLE != 0 && pre) {
-                        lds_wait_n<1>(nextv);  // younger: the previous block's row 2 write / consumed flag
-                        v = nextv;
-                    } else {
-                        if (ROLE != 0 && seen_ready < b + 1 && !(ABL & 1)) {
-                            seen_ready = spin_until_ge(ready_l + wv, b + 1);
-                            if (seen_ready < 0) { ok = false; return; }
-                        }
-                        v = lds_rd128(slot_row(wv, b, 0));
-                    }
-                    PT_END(pt_in);
-                } else {
-                    PT_BEGIN();
-                    if (!(ABL & 2)) lds_wait_n<WRITES ? 1 : 0>(nextv);  // younger: row S-1's write
-                    PT_END(pt_lds);
-                    v = (ABL & 2) ? fake : nextv;
-                }
-                if (ABL & 2) {
-                } else if (S < 2) {
-                    nextv = lds_rd128_issue(slot_row(wv, b, S + 1));
-                } else {
-                    pre = false;
-                    if (ROLE != 0 && b + 1 < nblk && seen_ready >= b + 2) {
-                        nextv = lds_rd128_issue(slot_row(wv, b + 1, 0));
-                        pre = true;
-                    }
-                    if (ROLE == 0) {
-                        if (!(ABL & 4) && b + NSI - 1 < nblk) stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);  // refills slot (b-1) % NSI
-                    } else if (lane == 0) {
-                        lds_wr32(consumed_l + wv, b + 1);
-                    }
-                }
-                cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
-                if (ROLE == 0 && wrap) {
-#pragma unroll
-                    for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
-                }
-#pragma unroll
-                for (int g = 0; g < KW; ++g) {
-                    if constexpr (VF) {
-                        if (S == 0) vstage<KW, DW, 0>(p, g, cur);
-                        if (S == 1) vstage<KW, DW, 1>(p, g, cur);
-                        if (S == 2) vstage<KW, DW, 2>(p, g, cur);
-                    } else {
-                        if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
-                        if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
-                        if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
-                    }
-                }
-                if constexpr (!WRITES) {
-                    const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                    if (!(ABL & 4)) store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
-                    srow += pitch_b;
-                    if (a.slots) {
-                        uint32_t c = 0;
-#pragma unroll
-                        for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
-                        alive += bitop3<0x80>(c, st_mask, row_ok ? 0xFFFFFFFFu : 0u);  // c & writer & row_ok
-                    }
-                } else {
-                    if (S == 0) {
-                        if (b > 0) {
-                            lds_wait1();  // all but the row-1 read: block b-1's row writes are done
-                            if (lane == 0) lds_wr32(ready_l + wv + 1, b);
-                        }
-                        if (seen_free < b + 1 - NS && !(ABL & 1)) {  // slot b % NS of ring wv+1 free: block b-NS consumed
-                            PT_BEGIN();
-                            seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
-                            PT_END(pt_free);
-                            if (seen_free < 0) { ok = false; return; }
-                        }
-                    }
-                    if (ABL & 2) fake = v4u32{cur[0], cur[1], cur[2], cur[3]} ^ fake;
-                    else lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
-                }
-            }
-        }
-        if (WRITES) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows written before the flag
-            if (lane == 0) lds_wr32(ready_l + wv + 1, nblk);
-        }
-    };
-    (void)ok;
-    if (wv == 0) role_loop(std::integral_constant<int, 0>());
-    else if (wv == P - 1) role_loop(std::integral_constant<int, 2>());
-    else role_loop(std::integral_constant<int, 1>());
-#else
-    for (int b = 0; b < nblk && ok; ++b) {
-        // input block b
-        PT_BEGIN();
-        if (wv == 0) {
-            // block b landed; blocks b+1 .. b+NSI-2 (if any) may stay in flight
-            const int inflight = min(NSI - 2, nblk - 1 - b);
-            if (inflight >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-            else if (inflight == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            else if (inflight == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (seen_ready < b + 1) {
-            seen_ready = (GOL_PIPE_ABL & 1) ? b + 1 : spin_until_ge(ready_l + wv, b + 1);
-            ok = seen_ready >= 0;
-            if (!ok) break;
-        }
-        PT_END(pt_in);
-        v4u32 nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, 0));
-#pragma unroll
-        for (int S = 0; S < 3; ++S) {
-            uint32_t cur[DW];
-            {
-                // wait on the issued register itself (a copy taken before the wait would read
-                // the VGPR while the ds_read is in flight); row S+1 is read while row S computes
-                PT_BEGIN();
-                if (!(GOL_PIPE_ABL & 2)) lds_wait(nextv);
-                PT_END(pt_lds);
-                const v4u32 v = nextv;
-                if (S < 2) nextv = (GOL_PIPE_ABL & 2) ? fake : lds_rd128_issue(slot_row(wv, b, S + 1));
-                cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
-            }
-            if (S == 2) {
-                if (wv == 0) {
-                    if (!(GOL_PIPE_ABL & 20) && b + NSI - 1 < nblk)
-                        stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);  // refills slot (b-1) % NSI
-                } else if (lane == 0) {
-                    lds_wr32(consumed_l + wv, b + 1);
-                }
-            }
-            if (wv == 0 && wrap) {
-#pragma unroll
-                for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
-            }
-#pragma unroll
-            for (int g = 0; g < KW; ++g) {
-                if constexpr (VF) {
-                    if (S == 0) vstage<KW, DW, 0>(p, g, cur);
-                    if (S == 1) vstage<KW, DW, 1>(p, g, cur);
-                    if (S == 2) vstage<KW, DW, 2>(p, g, cur);
-                } else {
-                    if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
-                    if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
-                    if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
-                }
-            }
-            if (wv == P - 1) {
-                const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                if (!(GOL_PIPE_ABL & 12)) store_row_masked<DW>(srow, row_ok ? row_bytes : 0u, st_off, cur);  // dropped unless row_ok
-                srow += pitch_b;
-                if (a.slots) {
-                    uint32_t c = 0;
-#pragma unroll
-                    for (int j = 0; j < DW; ++j) c += __popc(cur[j]);
-                    alive += bitop3<0x80>(c, st_mask, row_ok ? 0xFFFFFFFFu : 0u);  // c & writer & row_ok
-                }
-            } else {
-                if (S == 0 && seen_free < b + 1 - NS) {  // slot b % NS of ring wv+1 free: block b-NS consumed
-                    PT_BEGIN();
-                    seen_free = (GOL_PIPE_ABL & 1) ? b + 1 : spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
-                    PT_END(pt_free);
-                    ok = seen_free >= 0;
-                    if (!ok) break;
-                }
-                if (!(GOL_PIPE_ABL & 2)) lds_wr128(slot_row(wv + 1, b, S), v4u32{cur[0], cur[1], cur[2], cur[3]});
-                else fake = v4u32{cur[0], cur[1], cur[2], cur[3]} ^ fake;
-            }
-        }
-        if (ok && wv < P - 1) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows written before the flag
-            if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
-        }
-    }
-#endif
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if GOL_PIPE_PROFILE
-    // diagnostic build only: per-role cycle sums in slots[role*64 + 8*i] (i: total, input wait,
-    // free-slot wait, LDS row wait, waves)
-    if (lane == 0 && a.slots) {
-        unsigned long long *q = (unsigned long long *)a.slots + wv * 64;
-        atomicAdd(q + 0, (unsigned long long)(__builtin_amdgcn_s_memtime() - pt0));
-        atomicAdd(q + 8, (unsigned long long)pt_in);
-        atomicAdd(q + 16, (unsigned long long)pt_free);
-        atomicAdd(q + 24, (unsigned long long)pt_lds);
-        atomicAdd(q + 32, 1ull);
-    }
-    return;
-#endif
-    if (GOL_PIPE_ABL & 2) alive += fake.x & fake.y & fake.z & fake.w & 1u;  // keep the ablated compute alive
     if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
 
@@ -1405,8 +811,8 @@ __device__ __forceinline__ void transpose32(uint32_t (&x)[32])
 }
 
 // Standard bit rows (word s bit i = cell 32s + i) -> band rows, or back.  One lane per
-// (row, m): the 32 standard words m, m + Wm, ..., m + 31*Wm (Wm = Wd/32) hold exactly
-// the cells of band words 32m .. 32m+31, so the conversion is one 32x32 transpose.
+// (row, m): the 32 standard words m, m + Wm, ..., m + 31*Wm (Wm = Wd/32) hold exactly the
+// cells of band words 32m .. 32m+31, so the conversion is one 32x32 transpose.
 template <bool TO_BAND>
 __global__ void band_convert_kernel(const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wm, int64_t spitch,
                                     int64_t dpitch)
@@ -1441,10 +847,10 @@ __global__ void band_convert_kernel(const uint32_t *src, uint32_t *dst, int64_t 
 }
 
 // ------------------------------------------------------------------ byte-board step, k turns per launch
-// For boards whose bytes are all 0 or 255 (every board after its first turn):
-// each lane packs 32 bytes of a row into one 32-cell word (bit i = byte i & 1),
-// runs the same K-stage register pipeline as the bit board (shifted frame), and
-// unpacks the result to 0/255 bytes.  HBM traffic: 2 bytes per cell per K turns.
+// For boards whose bytes are all 0 or 255 (every board after its first turn): each lane
+// packs 32 bytes of a row into one 32-cell word (bit i = byte i & 1), runs the same K-stage
+// shifted-frame register pipeline as the standard bit board and unpacks the result to 0/255
+// bytes.  HBM traffic: 2 bytes per cell per K turns.
 __device__ __forceinline__ uint32_t pack32(const uint4 lo, const uint4 hi)
 {
     const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -1476,17 +882,15 @@ struct BytesKArgs {
     int64_t R, Wd, pitch, row0, rows;  // Wd = W / 32 words, pitch in bytes
     int32_t strip, ngroups;
     uint64_t *slots;
+    uint32_t *err;
 };
-
-#ifndef GOL_BYTES_PREFETCH
-#define GOL_BYTES_PREFETCH 1  // row blocks loaded ahead of use (raw bytes: 8 VGPRs per row; 3 measured slower)
-#endif
 
 // Byte rows of one lane: 32 bytes = two 16-byte loads, packed to a word at use.
 struct Raw32 {
     uint4 lo, hi;
 };
 
+// One wave = all K stages (k = 1..16), 62 column words per wave.
 template <int K>
 __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
 {
@@ -1500,8 +904,7 @@ __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
     const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
     const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
     const int first_in = s0 - K, last_in = s1 + K - 1;
-    constexpr int PF = GOL_BYTES_PREFETCH;
-    constexpr int NB = PF + 1;
+    constexpr int NB = 2;  // blocks per loop trip: one block loaded ahead
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
     const int nblk_r = (nblk + NB - 1) / NB * NB;  // trailing blocks store nothing
     // row addresses: a.mid + (segment displacement + y * pitch) (see band_step_kernel)
@@ -1525,20 +928,16 @@ __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
     auto store = [&](char *row, uint32_t nbytes, const uint32_t w) {
         uint4 lo, hi;
         unpack32(w, lo, hi);
-        const uint32_t v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, (int)nbytes, 0x00020000);
         typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{v[0], v[1], v[2], v[3]}, r, st_off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{v[4], v[5], v[6], v[7]}, r, st_off + 16u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{lo.x, lo.y, lo.z, lo.w}, r, st_off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, hi.z, hi.w}, r, st_off + 16u, 0, 0);
     };
-    typedef PipeSel<K, 1, 1> PS;
-    typename PS::type p;
-    PS::init(p);
+    Pipe<K, 1> p;
+    pipe_init(p);
     Raw32 ring[NB][3];
 #pragma unroll
-    for (int b = 0; b < PF; ++b)
-#pragma unroll
-        for (int s = 0; s < 3; ++s) load(first_in + 3 * b + s, ring[b][s]);
+    for (int s = 0; s < 3; ++s) load(first_in + s, ring[0][s]);
     // same memory-counter history on loop entry as on the back edge (3 rows x 2 stores)
 #pragma unroll
     for (int s = 0; s < 3; ++s) store(dst_b, 0u, 0u);
@@ -1548,15 +947,15 @@ __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
         for (int u = 0; u < NB; ++u) {
             const int t0 = (blk0 + u) * 3;
 #pragma unroll
-            for (int s = 0; s < 3; ++s) load(first_in + t0 + 3 * PF + s, ring[(u + PF) % NB][s]);
+            for (int s = 0; s < 3; ++s) load(first_in + t0 + 3 + s, ring[(u + 1) % NB][s]);
             uint32_t cur[3][1];
 #pragma unroll
             for (int s = 0; s < 3; ++s) cur[s][0] = pack32(ring[u][s].lo, ring[u][s].hi);
 #pragma unroll
             for (int w = 0; w < K + 2; ++w) {
-                if (w < K) PS::template stage<0>(p, w, cur[0]);
-                if (w >= 1 && w - 1 < K) PS::template stage<1>(p, w - 1, cur[1]);
-                if (w >= 2 && w - 2 < K) PS::template stage<2>(p, w - 2, cur[2]);
+                if (w < K) sstage<K, 1, 0>(p, w, cur[0]);
+                if (w >= 1 && w - 1 < K) sstage<K, 1, 1>(p, w - 1, cur[1]);
+                if (w >= 2 && w - 2 < K) sstage<K, 1, 2>(p, w - 2, cur[2]);
             }
 #pragma unroll
             for (int S = 0; S < 3; ++S) {
@@ -1592,25 +991,12 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
         : "memory");
 }
 
-#ifndef GOL_BYTES_PIPE_DEFER
-#define GOL_BYTES_PIPE_DEFER 1  // +2.8 % on byte16k (same-box A/B, profiles/r01_final/ab_defer.log)
-#endif
-#ifndef GOL_BYTES_PIPE_NB
-#define GOL_BYTES_PIPE_NB 1  // loader's raw byte blocks in registers (1: 67 VGPRs, 3 workgroups per CU; +13 % on byte16k)
-#endif
-#ifndef GOL_BYTES_PIPE_WPE
-#define GOL_BYTES_PIPE_WPE 0  // > 0: waves per SIMD the compiler must fit (occupancy experiment)
-#endif
 template <int KW, int P>
-__global__ void __launch_bounds__(64 * P)
-#if GOL_BYTES_PIPE_WPE > 0
-__attribute__((amdgpu_waves_per_eu(GOL_BYTES_PIPE_WPE)))
-#endif
-bytes_pipe_kernel(BytesKArgs a)
+__global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 {
     constexpr int K = KW * P;
     static_assert(K <= 32, "one 32-cell halo word per side");
-    constexpr int NS = GOL_PIPE_SLOTS;
+    constexpr int NS = 3;
     constexpr int ROW = 64;  // uint32 per LDS row
     __shared__ uint32_t ring[P - 1][NS][3][ROW];
     __shared__ int ready[P], consumed[P];
@@ -1661,32 +1047,27 @@ bytes_pipe_kernel(BytesKArgs a)
         return ring_l + (((e - 1) * NS + b % NS) * 3 + S) * ROW + lane;
     };
 
-    typedef PipeSel<KW, 1, 1> PS;
-    typename PS::type p;
-    PS::init(p);
-    // wave 0: raw bytes of the current and the next block in registers (8 VGPRs per row);
-    // NB = 1: one block, packed before the next block's loads are issued into it
-    constexpr int NB = GOL_BYTES_PIPE_NB;
-    Raw32 buf[NB][3];
+    Pipe<KW, 1> p;
+    pipe_init(p);
+    // wave 0: the raw bytes of one block in registers (8 VGPRs per row), packed to 3 words
+    // before the next block's loads are issued into the same registers
+    Raw32 buf[3];
     if (wv == 0) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) load(first_in + s, buf[0][s]);
+        for (int s = 0; s < 3; ++s) load(first_in + s, buf[s]);
     }
     uint32_t alive = 0;
     bool ok = true;
     int seen_ready = 0, seen_free = 0;
     const uint32_t nrows = (uint32_t)(s1 - s0);
     char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch;
-    auto block = [&](int b, auto par) {
-        constexpr int PAR = decltype(par)::value;  // wave 0's buffer of block b
+    auto block = [&](int b) {
         uint32_t rows3[3] = {0, 0, 0};
         if (wv == 0) {
-            if constexpr (NB == 1) {
 #pragma unroll
-                for (int s = 0; s < 3; ++s) rows3[s] = pack32(buf[0][s].lo, buf[0][s].hi);
-            }
+            for (int s = 0; s < 3; ++s) rows3[s] = pack32(buf[s].lo, buf[s].hi);
 #pragma unroll
-            for (int s = 0; s < 3; ++s) load(first_in + 3 * (b + 1) + s, buf[(1 - PAR) % NB][s]);  // clamped past the end
+            for (int s = 0; s < 3; ++s) load(first_in + 3 * (b + 1) + s, buf[s]);  // clamped past the end
         } else if (seen_ready < b + 1) {
             seen_ready = spin_until_ge(ready_l + wv, b + 1);
             ok = seen_ready >= 0;
@@ -1699,20 +1080,17 @@ bytes_pipe_kernel(BytesKArgs a)
             lds_rd32x3(slot_row(wv, b, 0), rows3);
             if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
         }
-#if GOL_BYTES_PIPE_DEFER
         // the three rows' stages first, one basic block the scheduler can interleave (stage g
         // of row S+1 is independent of stage g+1 of row S), then the stores / ring writes
         uint32_t outw[3];
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
-            uint32_t cur[1];
-            if (wv == 0 && NB == 2) cur[0] = pack32(buf[PAR % NB][S].lo, buf[PAR % NB][S].hi);
-            else cur[0] = rows3[S];
+            uint32_t cur[1] = {rows3[S]};
 #pragma unroll
             for (int g = 0; g < KW; ++g) {
-                if (S == 0) PS::template stage<0>(p, g, cur);
-                if (S == 1) PS::template stage<1>(p, g, cur);
-                if (S == 2) PS::template stage<2>(p, g, cur);
+                if (S == 0) sstage<KW, 1, 0>(p, g, cur);
+                if (S == 1) sstage<KW, 1, 1>(p, g, cur);
+                if (S == 2) sstage<KW, 1, 2>(p, g, cur);
             }
             outw[S] = cur[0];
         }
@@ -1720,6 +1098,8 @@ bytes_pipe_kernel(BytesKArgs a)
 #pragma unroll
             for (int S = 0; S < 3; ++S) {
                 const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
+                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
+                // takes its shift mod 32)
                 const uint32_t nx = from_upper_lane(outw[S]);
                 const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, outw[S], K % 32) : nx;
                 store(srow, row_ok ? row_bytes : 0u, o);
@@ -1735,48 +1115,18 @@ bytes_pipe_kernel(BytesKArgs a)
 #pragma unroll
             for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)outw[S]);
         }
-#else
-#pragma unroll
-        for (int S = 0; S < 3; ++S) {
-            uint32_t cur[1];
-            if (wv == 0 && NB == 2) cur[0] = pack32(buf[PAR % NB][S].lo, buf[PAR % NB][S].hi);
-            else cur[0] = rows3[S];
-#pragma unroll
-            for (int g = 0; g < KW; ++g) {
-                if (S == 0) PS::template stage<0>(p, g, cur);
-                if (S == 1) PS::template stage<1>(p, g, cur);
-                if (S == 2) PS::template stage<2>(p, g, cur);
-            }
-            if (wv == P - 1) {
-                const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
-                // takes its shift mod 32)
-                const uint32_t nx = from_upper_lane(cur[0]);
-                const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, cur[0], K % 32) : nx;
-                store(srow, row_ok ? row_bytes : 0u, o);
-                srow += pitch;
-                if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
-            } else {
-                if (S == 0 && seen_free < b + 1 - NS) {
-                    seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
-                    ok = seen_free >= 0;
-                    if (!ok) return;
-                }
-                lds_wr32(slot_row(wv + 1, b, S), (int)cur[0]);
-            }
-        }
-#endif
         if (wv < P - 1) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
         }
     };
     int b = 0;
-    for (; b + 1 < nblk && ok; b += 2) {
-        block(b, std::integral_constant<int, 0>());
-        if (ok) block(b + 1, std::integral_constant<int, 1>());
+    for (; b + 1 < nblk && ok; b += 2) {  // two blocks per trip (the measured schedule)
+        block(b);
+        if (ok) block(b + 1);
     }
-    if (b < nblk && ok) block(b, std::integral_constant<int, 0>());
+    if (b < nblk && ok) block(b);
+    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
     if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
 
@@ -1872,8 +1222,8 @@ __global__ void __launch_bounds__(256) bytes_step_kernel(BytesArgs a)
     }
 }
 
-// Scalar fallback for widths that are not a multiple of 16 (one thread per cell),
-// a literal restatement of worker.go:26-37 / 44-70.
+// Widths that are not a multiple of 16 (one thread per cell), a literal restatement of
+// worker.go:26-37 / 44-70.
 __global__ void bytes_step_scalar_kernel(BytesArgs a)
 {
     const int64_t n = (a.y1 - a.y0) * a.W;
@@ -1916,6 +1266,18 @@ __global__ void popcount_kernel(const uint32_t *src, int64_t rows, int64_t Wd, i
         c += __popc(src[y * pitch + w]);
     }
     slot_add(slots, c);
+}
+
+// Sum the GOL_COUNT_SLOTS slots of `n` consecutive slot arrays into out[0..n) (one wave each).
+__global__ void slots_reduce_kernel(const uint64_t *slots, int64_t n, uint64_t *out)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (i >= n) return;
+    uint64_t s = 0;
+    for (int j = lane; j < GOL_COUNT_SLOTS; j += 64) s += slots[(i * GOL_COUNT_SLOTS + j) * 8];
+    s = wave_sum_u64(s);
+    if (lane == 0) out[i] = s;
 }
 
 __global__ void hash_kernel(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Ww, int64_t pitch,
@@ -2006,12 +1368,12 @@ __global__ void unpack_kernel(const uint32_t *bits, int64_t rows, int64_t W, int
     }
 }
 
-// Alive-cell list, row-major (broker.go:47-58): one wave per row, ballot + mbcnt
-// prefix over 64 cells at a time.  offs[y] = first output index of row y.
-// With `prev` the listed cells are those that differ from `prev` (the CellFlipped events of
-// one turn, gol/event.go:50-60): the same kernels over bits ^ prev.
+// Alive-cell list, row-major (broker.go:47-58): one wave per row, ballot + mbcnt prefix over
+// 64 cells at a time.  offs[y] = first output index of row y.  With `prev` the listed cells
+// are those that differ from `prev` (the CellFlipped events of one turn,
+// gol/event.go:50-60): the same kernels over bits ^ prev.  y0 is the global row of row 0.
 __global__ void alive_list_bits_kernel(const uint32_t *bits, const uint32_t *prev, int64_t rows, int64_t Wd,
-                                       int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap)
+                                       int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, int64_t y0)
 {
     const int lane = threadIdx.x & 63;
     const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -2033,7 +1395,7 @@ __global__ void alive_list_bits_kernel(const uint32_t *bits, const uint32_t *pre
         while (m) {
             const int b = __ffs(m) - 1;
             m &= m - 1;
-            if (o < cap) { xy[2 * o] = (int32_t)(32 * w + b); xy[2 * o + 1] = (int32_t)y; }
+            if (o < cap) { xy[2 * o] = (int32_t)(32 * w + b); xy[2 * o + 1] = (int32_t)(y0 + y); }
             ++o;
         }
         base += __shfl(incl, 63, 64);
@@ -2048,7 +1410,7 @@ __device__ __forceinline__ bool byte_listed(const uint8_t *bytes, const uint8_t 
 }
 
 __global__ void alive_list_bytes_kernel(const uint8_t *bytes, const uint8_t *prev, int64_t rows, int64_t W,
-                                        int64_t stride, const int64_t *offs, int32_t *xy, int64_t cap)
+                                        int64_t stride, const int64_t *offs, int32_t *xy, int64_t cap, int64_t y0)
 {
     const int lane = threadIdx.x & 63;
     const int64_t y = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -2060,7 +1422,7 @@ __global__ void alive_list_bytes_kernel(const uint8_t *bytes, const uint8_t *pre
         const uint64_t m = __ballot(alive);
         if (alive) {
             const int64_t o = base + __popcll(m & ((1ULL << lane) - 1));
-            if (o < cap) { xy[2 * o] = (int32_t)x; xy[2 * o + 1] = (int32_t)y; }
+            if (o < cap) { xy[2 * o] = (int32_t)x; xy[2 * o + 1] = (int32_t)(y0 + y); }
         }
         base += __popcll(m);
     }
@@ -2106,45 +1468,58 @@ static inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 16)
     return (int)g;
 }
 
-template <int K, int DW, int ALGO>
+// Per-device error word used when a launcher is called without one (gol_dev_* launchers).
+uint32_t *golk_device_err_word(int device)
+{
+    static std::mutex mu;
+    static std::map<int, uint32_t *> words;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = words.find(device);
+    if (it != words.end()) return it->second;
+    int prev = 0;
+    uint32_t *w = nullptr;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return nullptr;
+    if (hipMalloc(&w, sizeof(uint32_t)) != hipSuccess || hipMemset(w, 0, sizeof(uint32_t)) != hipSuccess) w = nullptr;
+    (void)hipSetDevice(prev);
+    if (w) words[device] = w;
+    return w;
+}
+
+static uint32_t *err_or_default(uint32_t *err)
+{
+    if (err) return err;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    return golk_device_err_word(dev);
+}
+
+template <int K, int DW>
 static hipError_t launch_bits(const BitsArgs &a, hipStream_t s)
 {
     const int nstrips = (int)((a.rows + a.strip - 1) / a.strip);
     dim3 grid((a.ngroups + 3) / 4, nstrips);
-    hipLaunchKernelGGL((bits_step_kernel<K, DW, ALGO>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((bits_step_kernel<K, DW>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-template <int DW, int ALGO>
+template <int DW>
 static hipError_t launch_bits_k(int k, const BitsArgs &a, hipStream_t s)
 {
     switch (k) {
-    case 1: return launch_bits<1, DW, ALGO>(a, s);
-    case 2: return launch_bits<2, DW, ALGO>(a, s);
-    case 4: return launch_bits<4, DW, ALGO>(a, s);
-    case 8: return launch_bits<8, DW, ALGO>(a, s);
-    case 16: if constexpr (DW <= 2) return launch_bits<16, DW, ALGO>(a, s);
+    case 1: return launch_bits<1, DW>(a, s);
+    case 2: return launch_bits<2, DW>(a, s);
+    case 4: return launch_bits<4, DW>(a, s);
+    case 8: return launch_bits<8, DW>(a, s);
+    case 16: if constexpr (DW <= 2) return launch_bits<16, DW>(a, s);
              return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
     }
 }
 
-// Step formulation: 0 = centred horizontal sums, 1 = shifted frame (left neighbours only).
-// GOL_BITS_ALGO overrides the default (used by tools/sweep.py).
-int golk_bits_algo()
-{
-    static int algo = [] {
-        const char *e = getenv("GOL_BITS_ALGO");
-        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : GOL_DEFAULT_ALGO;
-    }();
-    return algo;
-}
-
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
 {
-    // aim for >= ~8192 waves (32 per CU) but no longer than 64*k rows: the 2k halo rows
-    // then cost <= 1/32 (measured best on the 2^17 x 2^20 torus: 512 rows at k = 8,
-    // 1024 at k = 16)
+    // aim for >= ~8192 waves (32 per CU) but no longer than 64*k rows: the 2k halo rows then
+    // cost <= 1/32 (measured best on the 2^17 x 2^20 torus: 512 rows at k = 8, 1024 at k = 16)
     int64_t strip = rows * ngroups / 8192;
     const int64_t hi = 64 * (int64_t)k;
     if (strip > hi) strip = hi;
@@ -2160,25 +1535,25 @@ int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
 static int64_t resident_workgroups(const void *kernel, int block)
 {
     static std::mutex mu;
-    static std::map<const void *, int64_t> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(kernel);
-    if (it != cache.end()) return it->second;
+    static std::map<std::pair<const void *, int>, int64_t> cache;
     int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({kernel, dev});
+    if (it != cache.end()) return it->second;
     int64_t n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) == hipSuccess)
         n = (int64_t)cus * per_cu;
-    cache[kernel] = n;
+    cache[{kernel, dev}] = n;
     return n;
 }
 
-// Strip length for a one-workgroup-per-(column group, strip) kernel on a board that fills
-// the device only a few times over: the strip count is a multiple of the strips that fit
-// in one round of resident workgroups, so the last round is not a small remainder (e.g.
-// 65536^2 at k = 12: 9 groups x 228 strips = 2052 workgroups was 2 rounds + 4 workgroups).
-// Boards of many rounds keep `fallback` (their tail is a small fraction already).
+// Strip length for a one-workgroup-per-(column group, strip) kernel on a board that fills the
+// device only a few times over: the strip count is a multiple of the strips that fit in one
+// round of resident workgroups, so the last round is not a small remainder (e.g. 65536^2 at
+// k = 12: 9 groups x 228 strips = 2052 workgroups was 2 rounds + 4 workgroups).  Boards of
+// many rounds keep `fallback` (their tail is a small fraction already).
 static int64_t round_tiled_strip(int64_t rows, int64_t ngroups, int64_t slots, int64_t min_rows, int64_t cap,
                                  int64_t fallback)
 {
@@ -2201,36 +1576,14 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.ngroups = (int)((Wd + 62 * dw - 1) / (62 * dw));
     a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
     a.slots = slots;
+    a.err = nullptr;  // no flag waits in this kernel
     if (rows <= 0) return hipSuccess;
-    const int algo = golk_bits_algo();
-    switch (dw * 2 + algo) {
-    case 2: return launch_bits_k<1, 0>(k, a, s);
-    case 3: return launch_bits_k<1, 1>(k, a, s);
-    case 4: return launch_bits_k<2, 0>(k, a, s);
-    case 5: return launch_bits_k<2, 1>(k, a, s);
-    case 8: return launch_bits_k<4, 0>(k, a, s);
-    case 9: return launch_bits_k<4, 1>(k, a, s);
+    switch (dw) {
+    case 1: return launch_bits_k<1>(k, a, s);
+    case 2: return launch_bits_k<2>(k, a, s);
+    case 4: return launch_bits_k<4>(k, a, s);
     default: return hipErrorInvalidValue;
     }
-}
-
-// Vertical-first band kernel (4 words per lane): k = 8, 12 or 16 in one wave.
-template <bool C>
-static hipError_t launch_band_vf(int k, dim3 grid, const BitsArgs &a, hipStream_t s)
-{
-    // GOL_BAND_LDS_PAD (bytes of unused dynamic LDS per workgroup) caps the workgroups per
-    // CU: an occupancy experiment knob (measurement only)
-    static const size_t pad = [] {
-        const char *e = getenv("GOL_BAND_LDS_PAD");
-        return e ? (size_t)atol(e) : (size_t)0;
-    }();
-    switch (k) {
-    case 8: hipLaunchKernelGGL((band_step_kernel<8, 4, C, true>), grid, dim3(256), pad, s, a); break;
-    case 12: hipLaunchKernelGGL((band_step_kernel<12, 4, C, true>), grid, dim3(256), pad, s, a); break;
-    case 16: hipLaunchKernelGGL((band_step_kernel<16, 4, C, true>), grid, dim3(256), pad, s, a); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
 }
 
 template <int DW, bool C>
@@ -2248,111 +1601,46 @@ static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s
     return hipGetLastError();
 }
 
-template <int KW, int P>
-static hipError_t launch_band_split(bool contig, BitsArgs a, hipStream_t s, bool auto_strip = false)
+// k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
+static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
+    constexpr int KW = 3, P = 4;
     if (auto_strip) {
         const void *kf = contig ? (const void *)band_pipe_kernel<KW, P, true> : (const void *)band_pipe_kernel<KW, P, false>;
         a.strip = (int)round_tiled_strip(a.rows, a.ngroups, resident_workgroups(kf, 64 * P), 8 * KW * P, 1024, a.strip);
     }
     const dim3 grid(a.ngroups, (int)((a.rows + a.strip - 1) / a.strip));
-    static const int sync = [] {  // 1 = LDS flags (default), 0 = one workgroup barrier per block
-        const char *e = getenv("GOL_SPLIT_SYNC");
-        return e ? atoi(e) : 1;
-    }();
-    if (sync) {
-        if (contig)
-            hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), grid, dim3(64 * P), 0, s, a);
-        else
-            hipLaunchKernelGGL((band_pipe_kernel<KW, P, false>), grid, dim3(64 * P), 0, s, a);
-    } else {
-        if (contig)
-            hipLaunchKernelGGL((band_split_kernel<KW, P, true>), grid, dim3(64 * P), 0, s, a);
-        else
-            hipLaunchKernelGGL((band_split_kernel<KW, P, false>), grid, dim3(64 * P), 0, s, a);
-    }
-    return hipGetLastError();
-}
-
-// Vertical-first split pipeline: k = KW * P (VF stages hold 2 VGPRs per word and stage).
-template <int KW, int P>
-static hipError_t launch_band_pipe_vf(bool contig, const BitsArgs &a, hipStream_t s)
-{
-    const dim3 grid(a.ngroups, (int)((a.rows + a.strip - 1) / a.strip));
     if (contig)
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), grid, dim3(64 * P), 0, s, a);
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), grid, dim3(64 * P), 0, s, a);
     else
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), grid, dim3(64 * P), 0, s, a);
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false>), grid, dim3(64 * P), 0, s, a);
     return hipGetLastError();
-}
-
-// Split-pipeline band step (k = 4 * waves per workgroup, 4 words per lane): 0 = off.
-int golk_band_split_enabled()
-{
-    static int on = [] {
-        const char *e = getenv("GOL_BAND_SPLIT");
-        return e ? atoi(e) : GOL_BAND_SPLIT_DEFAULT;
-    }();
-    return on;
 }
 
 hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
-                          uint64_t *slots, hipStream_t s)
+                          uint64_t *slots, uint32_t *err, hipStream_t s)
 {
     if (rows <= 0) return hipSuccess;
-    static const int vf = [] {  // vertical-first one-wave kernel for 4 words per lane
-        const char *e = getenv("GOL_BAND_VF");
-        return e ? atoi(e) : GOL_BAND_VF_DEFAULT;
-    }();
-    if (vf && dw == 4 && (k == 8 || k == 12 || k == 16)) {
-        BitsArgs a;
-        a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
-        a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
-        const int U = band_useful_words(k, 4);
-        a.ngroups = (int)((Wd + U - 1) / U);
-        a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
-        a.slots = slots;
-        const dim3 grid((a.ngroups + 3) / 4, (int)((rows + a.strip - 1) / a.strip));
-        const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
-        return contig ? launch_band_vf<true>(k, grid, a, s) : launch_band_vf<false>(k, grid, a, s);
-    }
-    if (dw == 4 && (k == 12 || k == 24 || (golk_band_split_enabled() && (k == 8 || k == 16)))) {
-        BitsArgs a;
-        a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
-        a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
-        const int U = band_useful_words(k, 4);
-        a.ngroups = (int)((Wd + U - 1) / U);
+    BitsArgs a;
+    a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
+    a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
+    a.slots = slots;
+    a.err = err_or_default(err);
+    if (!a.err) return hipErrorOutOfMemory;
+    const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
+    const int U = band_useful_words(k, dw);
+    a.ngroups = (int)((Wd + U - 1) / U);
+    if (dw == 4 && k == 12) {
         // one workgroup per (column group, strip): strips up to 1024 rows (measured best at k = 12)
         a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP)
                             : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(1024, rows * a.ngroups / 2048)));
         // the pipe kernel's stores address a strip as one buffer (32-bit range)
         a.strip = (int)std::max<int64_t>(1, std::min<int64_t>(a.strip, (int64_t(1) << 30) / (pitch * 4)));
-        const bool auto_strip = strip <= 0;
-        a.slots = slots;
-        const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
-        if (k == 8) return launch_band_split<GOL_SPLIT_KW == 4 ? 4 : 2, GOL_SPLIT_KW == 4 ? 2 : 4>(contig, a, s);
-        if (k == 12 && GOL_PIPE_VF_DEFAULT) return launch_band_pipe_vf<12 / GOL_PIPE_VF_P, GOL_PIPE_VF_P>(contig, a, s);
-        if (k == 12) {
-            static const int shape = [] {  // waves per workgroup for k = 12 (measurement knob)
-                const char *e = getenv("GOL_PIPE_WAVES");
-                return e ? atoi(e) : 12 / GOL_SPLIT_KW;
-            }();
-            if (shape == 3) return launch_band_split<4, 3>(contig, a, s, auto_strip);
-            return launch_band_split<GOL_SPLIT_KW, 12 / GOL_SPLIT_KW>(contig, a, s, auto_strip);
-        }
-        if (k == 24) return launch_band_split<3, 8>(contig, a, s, auto_strip);  // 8 waves x 3 stages
-        return launch_band_split<4, 4>(contig, a, s);
+        return launch_band_pipe(contig, a, s, strip <= 0);
     }
-    BitsArgs a;
-    a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
-    a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
-    const int U = band_useful_words(k, dw);
-    a.ngroups = (int)((Wd + U - 1) / U);
     a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
-    a.slots = slots;
     dim3 grid((a.ngroups + 3) / 4, (int)((rows + a.strip - 1) / a.strip));
-    const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
     if (dw == 2) return contig ? launch_band<2, true>(k, grid, a, s) : launch_band<2, false>(k, grid, a, s);
     if (dw == 4) return contig ? launch_band<4, true>(k, grid, a, s) : launch_band<4, false>(k, grid, a, s);
     return hipErrorInvalidValue;
@@ -2364,6 +1652,7 @@ hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, i
                              int64_t spitch, int64_t dpitch, hipStream_t s)
 {
     const int64_t Wm = Wd / 32;
+    if (rows <= 0) return hipSuccess;
     const dim3 g(grid_for(rows * Wm, 256, 256 * 64));
     if (to_band)
         hipLaunchKernelGGL(band_convert_kernel<true>, g, dim3(256), 0, s, src, dst, rows, Wm, spitch, dpitch);
@@ -2400,7 +1689,7 @@ hipError_t golk_bytes_step(const uint8_t *world, int64_t H, int64_t W, int64_t s
 
 hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint8_t *bot, uint8_t *dst, int64_t R,
                               int64_t W, int64_t pitch, int64_t row0, int64_t rows, int k, int strip, uint64_t *slots,
-                              hipStream_t s)
+                              uint32_t *err, hipStream_t s)
 {
     BytesKArgs a;
     a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
@@ -2408,25 +1697,22 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
     a.ngroups = (int)((a.Wd + 61) / 62);
     a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
     a.slots = slots;
+    a.err = err_or_default(err);
     if (rows <= 0) return hipSuccess;
-    const int nstrips = (int)((rows + a.strip - 1) / a.strip);
-    dim3 grid((a.ngroups + 3) / 4, nstrips);
-    static const int bpipe = [] {  // 1: k = 16 on the 4-wave byte pipeline too
-        const char *e = getenv("GOL_BYTES_PIPE16");
-        return e ? atoi(e) : 0;
-    }();
-    if (k == 32 || (k == 16 && bpipe)) {
-        // one workgroup of k/4 waves per (column group, strip); strips >= 8k rows
+    if (!a.err) return hipErrorOutOfMemory;
+    if (k == 32) {
+        // one workgroup of 8 waves per (column group, strip), round-tiled strips >= 4k rows
         if (strip <= 0) {
             a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
-            const void *kf = k == 32 ? (const void *)bytes_pipe_kernel<4, 8> : (const void *)bytes_pipe_kernel<4, 4>;
-            a.strip = (int)round_tiled_strip(rows, a.ngroups, resident_workgroups(kf, 16 * k), 4 * k, 1024, a.strip);
+            a.strip = (int)round_tiled_strip(rows, a.ngroups, resident_workgroups((const void *)bytes_pipe_kernel<4, 8>, 512),
+                                             4 * k, 1024, a.strip);
         }
         const dim3 g2(a.ngroups, (int)((rows + a.strip - 1) / a.strip));
-        if (k == 32) hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), g2, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((bytes_pipe_kernel<4, 4>), g2, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), g2, dim3(512), 0, s, a);
         return hipGetLastError();
     }
+    const int nstrips = (int)((rows + a.strip - 1) / a.strip);
+    dim3 grid((a.ngroups + 3) / 4, nstrips);
     switch (k) {
     case 1: hipLaunchKernelGGL(bytes_blocked_kernel<1>, grid, dim3(256), 0, s, a); break;
     case 2: hipLaunchKernelGGL(bytes_blocked_kernel<2>, grid, dim3(256), 0, s, a); break;
@@ -2440,6 +1726,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
 
 hipError_t golk_nonbinary(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *flag, hipStream_t s)
 {
+    if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(nonbinary_kernel, dim3(grid_for(rows * W, 256, 256 * 16)), dim3(256), 0, s, bytes, rows, W, stride,
                        flag);
     return hipGetLastError();
@@ -2449,6 +1736,7 @@ hipError_t golk_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t 
                             hipStream_t s)
 {
     const int64_t Ww = W / 64;
+    if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(random_fill_kernel, dim3(grid_for(rows * Ww, 256, 256 * 64)), dim3(256), 0, s, dst, rows,
                        grow0, Ww, pitch, seed);
     return hipGetLastError();
@@ -2458,6 +1746,13 @@ hipError_t golk_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t 
 {
     hipLaunchKernelGGL(popcount_kernel, dim3(grid_for(rows * Wd, 256, 256 * 16)), dim3(256), 0, s, src, rows, Wd,
                        pitch, slots);
+    return hipGetLastError();
+}
+
+hipError_t golk_slots_reduce(const uint64_t *slots, int64_t n, uint64_t *out, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(slots_reduce_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, slots, n, out);
     return hipGetLastError();
 }
 
@@ -2480,6 +1775,7 @@ hipError_t golk_count_bytes(const uint8_t *src, int64_t rows, int64_t W, int64_t
 hipError_t golk_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stride, uint32_t *bits, int64_t pitch,
                      uint32_t *nonbinary, hipStream_t s)
 {
+    if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(pack_kernel, dim3(grid_for(rows * (W / 32), 256, 256 * 64)), dim3(256), 0, s, bytes, rows, W,
                        stride, bits, pitch, nonbinary);
     return hipGetLastError();
@@ -2488,6 +1784,7 @@ hipError_t golk_pack(const uint8_t *bytes, int64_t rows, int64_t W, int64_t stri
 hipError_t golk_unpack(const uint32_t *bits, int64_t rows, int64_t W, int64_t pitch, uint8_t *bytes, int64_t stride,
                        hipStream_t s)
 {
+    if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(unpack_kernel, dim3(grid_for(rows * (W / 32), 256, 256 * 64)), dim3(256), 0, s, bits, rows, W,
                        pitch, bytes, stride);
     return hipGetLastError();
@@ -2497,6 +1794,7 @@ hipError_t golk_row_counts(bool bits_mode, const void *board, const void *prev, 
                            int64_t pitch, int64_t *out, hipStream_t s)
 {
     const int wpb = 4;
+    if (rows <= 0) return hipSuccess;
     dim3 grid((unsigned)((rows + wpb - 1) / wpb));
     if (bits_mode)
         hipLaunchKernelGGL(row_counts_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board,
@@ -2508,15 +1806,16 @@ hipError_t golk_row_counts(bool bits_mode, const void *board, const void *prev, 
 }
 
 hipError_t golk_alive_list(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
-                           int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, hipStream_t s)
+                           int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, int64_t y0, hipStream_t s)
 {
     const int wpb = 4;
+    if (rows <= 0) return hipSuccess;
     dim3 grid((unsigned)((rows + wpb - 1) / wpb));
     if (bits_mode)
         hipLaunchKernelGGL(alive_list_bits_kernel, grid, dim3(64 * wpb), 0, s, (const uint32_t *)board,
-                           (const uint32_t *)prev, rows, width_units, pitch, offs, xy, cap);
+                           (const uint32_t *)prev, rows, width_units, pitch, offs, xy, cap, y0);
     else
         hipLaunchKernelGGL(alive_list_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board,
-                           (const uint8_t *)prev, rows, width_units, pitch, offs, xy, cap);
+                           (const uint8_t *)prev, rows, width_units, pitch, offs, xy, cap, y0);
     return hipGetLastError();
 }

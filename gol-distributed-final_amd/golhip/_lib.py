@@ -10,8 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# GOLHIP_LIB selects an alternative build of the same library (kernel experiments in tools/).
-LIB_PATH = os.environ.get("GOLHIP_LIB") or os.path.join(_HERE, "libgolhip.so")
+LIB_PATH = os.path.join(_HERE, "libgolhip.so")
 
 GOL_OK = 0
 GOL_EINVAL = -1
@@ -21,13 +20,19 @@ GOL_EIO = -4
 GOL_EFORMAT = -5
 GOL_ESTATE = -6
 GOL_EQUIT = -7
+GOL_ECOMM = -8
 GOL_COUNT_SLOTS = 256
+GOL_RCCL_ID_BYTES = 128
 GOL_LAYOUT_AUTO, GOL_LAYOUT_STANDARD, GOL_LAYOUT_BAND = 0, 1, 2
 LAYOUTS = {"auto": GOL_LAYOUT_AUTO, "standard": GOL_LAYOUT_STANDARD, "band": GOL_LAYOUT_BAND}
+GOL_TRANSPORT_AUTO, GOL_TRANSPORT_LOOPBACK, GOL_TRANSPORT_RCCL, GOL_TRANSPORT_LOCAL = 0, 1, 2, 3
+TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "rccl": GOL_TRANSPORT_RCCL}
+TRANSPORT_NAMES = {GOL_TRANSPORT_LOOPBACK: "loopback", GOL_TRANSPORT_RCCL: "rccl", GOL_TRANSPORT_LOCAL: "local"}
+GOL_SHARDS_SAME_DEVICE = 1
 
 _NAMES = {
     GOL_EINVAL: "EINVAL", GOL_EHIP: "EHIP", GOL_ENOMEM: "ENOMEM", GOL_EIO: "EIO",
-    GOL_EFORMAT: "EFORMAT", GOL_ESTATE: "ESTATE", GOL_EQUIT: "EQUIT",
+    GOL_EFORMAT: "EFORMAT", GOL_ESTATE: "ESTATE", GOL_EQUIT: "EQUIT", GOL_ECOMM: "ECOMM",
 }
 
 
@@ -40,7 +45,8 @@ class GolError(RuntimeError):
 class gol_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
                 ("strip_rows", ctypes.c_int32), ("cells_per_lane", ctypes.c_int32),
-                ("layout", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("layout", ctypes.c_int32), ("shards", ctypes.c_int32), ("transport", ctypes.c_int32),
+                ("flags", ctypes.c_int32)]
 
 
 class gol_request(ctypes.Structure):
@@ -72,19 +78,28 @@ SIGNATURES = [
     ("gol_next_state_slab", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64]),
     ("gol_partition_rows", ctypes.c_int, [_i64, _i64, _i64, _P(_i64), _P(_i64)]),
     ("gol_engine_create", ctypes.c_int, [_i64, _i64, _P(gol_config), _P(_vp)]),
+    ("gol_rccl_unique_id", ctypes.c_int, [_vp, _i64]),
+    ("gol_engine_create_rank", ctypes.c_int, [_i64, _i64, _i32, _i32, _vp, _P(gol_config), _P(_vp)]),
     ("gol_engine_destroy", None, [_vp]),
+    ("gol_engine_topology", ctypes.c_int, [_vp, _P(_i32), _P(_i32), _P(_i32), _P(_i32)]),
+    ("gol_engine_shard", ctypes.c_int, [_vp, _i32, _P(_i32), _P(_i64), _P(_i64)]),
     ("gol_engine_load_bytes", ctypes.c_int, [_vp, _vp, _i64]),
+    ("gol_engine_load_pgm", ctypes.c_int, [_vp, ctypes.c_char_p]),
     ("gol_engine_load_random", ctypes.c_int, [_vp, _u64]),
     ("gol_engine_step", ctypes.c_int, [_vp, _i64]),
+    ("gol_engine_step_counted", ctypes.c_int, [_vp, _i64, _i64, _vp, _i64]),
     ("gol_engine_turn", ctypes.c_int, [_vp, _P(_i64)]),
     ("gol_engine_alive_count", ctypes.c_int, [_vp, _P(_u64)]),
     ("gol_engine_store_bytes", ctypes.c_int, [_vp, _vp, _i64]),
+    ("gol_engine_store_rows", ctypes.c_int, [_vp, _i64, _i64, _vp, _i64]),
     ("gol_engine_alive_cells", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
     ("gol_engine_step_flips", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
     ("gol_engine_write_pgm", ctypes.c_int, [_vp, ctypes.c_char_p]),
     ("gol_engine_hash", ctypes.c_int, [_vp, _P(_u64)]),
     ("gol_engine_info", ctypes.c_int, [_vp, _P(_i32), _P(_i32), _P(_i32), _P(_i32)]),
     ("gol_engine_device_bits", ctypes.c_int, [_vp, _P(_vp), _P(_i64)]),
+    ("gol_engine_set_timing", ctypes.c_int, [_vp, _i32]),
+    ("gol_engine_timing", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double), _P(ctypes.c_double)]),
     ("gol_dev_bits_step", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
     ("gol_dev_random_fill", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _u64, _vp]),
@@ -99,6 +114,7 @@ SIGNATURES = [
      [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
     ("gol_band_max_k", ctypes.c_int, [_i32]),
     ("gol_dev_band_convert", ctypes.c_int, [_i32, _vp, _vp, _i64, _i64, _i64, _i64, _vp]),
+    ("gol_dev_error", ctypes.c_int, [_i32, _P(ctypes.c_uint32)]),
     ("gol_broker_create", ctypes.c_int, [_P(gol_config), _P(_vp)]),
     ("gol_broker_destroy", None, [_vp]),
     ("gol_broker_run", ctypes.c_int, [_vp, _P(gol_request), _P(gol_response)]),
@@ -113,19 +129,36 @@ SIGNATURES = [
 _lib = None
 
 
+def _one_hip_runtime():
+    """libgolhip.so links ROCm's libamdhip64.so.7; PyTorch ships its own copy with the same soname.
+    The first one loaded serves the whole process, and torch's GPU initialisation fails on the
+    other one, so torch (when installed) is loaded first: then both use torch's runtime (the two
+    are ABI-compatible: every GPU test passes torch tensors to the library)."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def load(path: str):
+    """Bind the C ABI of the shared object at `path` (raises if it is missing)."""
+    _one_hip_runtime()
+    if not os.path.exists(path):
+        raise GolError(GOL_ESTATE, f"{path} is missing: run __graft_entry__.build() "
+                                   "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib():
-    """Load libgolhip.so (raises if it has not been built)."""
+    """libgolhip.so, the product library (built in-tree next to this file)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise GolError(GOL_ESTATE, f"{LIB_PATH} is missing: run __graft_entry__.build() "
-                                       "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-        L = ctypes.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES:
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = load(LIB_PATH)
     return _lib
 
 

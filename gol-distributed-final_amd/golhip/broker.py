@@ -11,7 +11,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import check, gol_config, gol_request, gol_response, lib
+from ._lib import TRANSPORTS, check, gol_config, gol_request, gol_response, lib
 from .stubs import Cell, Request, Response
 
 
@@ -19,6 +19,11 @@ def _request(req: Request, keep: list) -> gol_request:
     r = gol_request()
     if req.World is not None:
         world = np.ascontiguousarray(req.World, dtype=np.uint8)
+        if world.ndim != 2 or world.shape != (req.ImageHeight, req.ImageWidth):
+            # the reference indexes World[y][x] for y < ImageHeight, x < ImageWidth and would
+            # panic on a smaller board (broker.go:67-70, 96-105)
+            raise ValueError(f"World has shape {world.shape}, expected (ImageHeight, ImageWidth) = "
+                             f"{(req.ImageHeight, req.ImageWidth)}")
         keep.append(world)
         r.World = world.ctypes.data
         r.world_stride = world.shape[1]
@@ -34,8 +39,12 @@ def _cells(xy: np.ndarray, n: int) -> list:
 class Operations:
     """broker.go:60 `type Operations struct{}` with its five RPC methods."""
 
-    def __init__(self, *, device: int = -1, turns_per_launch: int = 0, cells_per_lane: int = 0):
-        cfg = gol_config(device=device, turns_per_launch=turns_per_launch, cells_per_lane=cells_per_lane)
+    def __init__(self, *, device: int = -1, turns_per_launch: int = 0, cells_per_lane: int = 0, shards: int = 1,
+                 transport: str = "auto", same_device: bool = False):
+        """shards > 1: the board of a Run is row-sharded over that many GPUs (the reference's
+        Threads split, broker.go:135-206, applied to GPUs), with the same results."""
+        cfg = gol_config(device=device, turns_per_launch=turns_per_launch, cells_per_lane=cells_per_lane,
+                         shards=shards, transport=TRANSPORTS[transport], flags=1 if same_device else 0)
         h = ctypes.c_void_p()
         check(lib().gol_broker_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

@@ -1,8 +1,12 @@
-"""A Game-of-Life board resident on one MI355X (ctypes wrapper of gol_engine_*).
+"""A Game-of-Life board resident in HBM (ctypes wrapper of gol_engine_*).
 
 Replaces the broker's per-turn board handling (broker.go:62-234): the board is
 loaded once into HBM and stepped in k-turn kernel launches; queries (alive
 count, alive list, the board bytes, a PGM snapshot) are served from the device.
+The board may be row-sharded over several GPUs (broker.go:135-206's partition
+applied to GPUs) with a k-row halo exchange per launch: `shards=` in one process
+(RCCL between distinct GPUs, device copies between shards sharing a GPU), or
+`Engine.rank(...)` with one process per GPU (RCCL).
 """
 from __future__ import annotations
 
@@ -10,23 +14,53 @@ import ctypes
 
 import numpy as np
 
-from ._lib import LAYOUTS, check, gol_config, lib
+from ._lib import (GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, LAYOUTS, TRANSPORT_NAMES, TRANSPORTS, GolError,
+                   check, gol_config, lib)
+
+
+def rccl_unique_id(library=None) -> bytes:
+    """A fresh RCCL unique id (gol_rccl_unique_id) for Engine.rank; share it with every rank."""
+    L = library or lib()
+    buf = (ctypes.c_uint8 * GOL_RCCL_ID_BYTES)()
+    rc = L.gol_rccl_unique_id(buf, GOL_RCCL_ID_BYTES)
+    if rc:
+        raise GolError(rc, L.gol_last_error().decode(errors="replace"))
+    return bytes(buf)
 
 
 class Engine:
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
-                 strip_rows: int = 0, device: int = -1, layout: str = "auto"):
+                 strip_rows: int = 0, device: int = -1, layout: str = "auto", shards: int = 1,
+                 transport: str = "auto", same_device: bool = False, library=None, _rank=None):
         self.H, self.W = int(height), int(width)
+        self._L = library or lib()
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, strip_rows=strip_rows,
-                         cells_per_lane=cells_per_lane, layout=LAYOUTS[layout])
+                         cells_per_lane=cells_per_lane, layout=LAYOUTS[layout], shards=shards,
+                         transport=TRANSPORTS[transport], flags=GOL_SHARDS_SAME_DEVICE if same_device else 0)
         h = ctypes.c_void_p()
-        check(lib().gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))
+        if _rank is None:
+            self._check(self._L.gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))
+        else:
+            nranks, rank, uid = _rank
+            idbuf = (ctypes.c_uint8 * GOL_RCCL_ID_BYTES).from_buffer_copy(uid) if uid is not None else None
+            self._check(self._L.gol_engine_create_rank(self.H, self.W, nranks, rank, idbuf, ctypes.byref(cfg),
+                                                       ctypes.byref(h)))
         self._h = h
+
+    @classmethod
+    def rank(cls, height: int, width: int, nranks: int, rank: int, uid: bytes | None, **kw) -> "Engine":
+        """This process's shard `rank` of an `nranks`-rank board (one process per GPU, RCCL halo
+        exchange; collective: every rank constructs it with the same uid)."""
+        return cls(height, width, _rank=(nranks, rank, uid), **kw)
+
+    def _check(self, rc: int) -> None:
+        if rc:
+            raise GolError(rc, self._L.gol_last_error().decode(errors="replace"))
 
     # -- lifetime
     def close(self) -> None:
         if getattr(self, "_h", None) and self._h.value:
-            lib().gol_engine_destroy(self._h)
+            self._L.gol_engine_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):
@@ -46,32 +80,48 @@ class Engine:
         world = np.ascontiguousarray(world, dtype=np.uint8)
         if world.shape != (self.H, self.W):
             raise ValueError(f"board shape {world.shape} != {(self.H, self.W)}")
-        check(lib().gol_engine_load_bytes(self._h, world.ctypes.data, self.W))
+        self._check(self._L.gol_engine_load_bytes(self._h, world.ctypes.data, self.W))
 
     def load_random(self, seed: int) -> None:
-        check(lib().gol_engine_load_random(self._h, seed))
+        self._check(self._L.gol_engine_load_random(self._h, seed))
+
+    def load_pgm(self, path: str) -> None:
+        """readPgmImage (gol/io.go:90-126): every shard streams its own rows of the file."""
+        self._check(self._L.gol_engine_load_pgm(self._h, path.encode()))
 
     def store_bytes(self) -> np.ndarray:
         out = np.empty((self.H, self.W), dtype=np.uint8)
-        check(lib().gol_engine_store_bytes(self._h, out.ctypes.data, self.W))
+        self._check(self._L.gol_engine_store_bytes(self._h, out.ctypes.data, self.W))
+        return out
+
+    def store_rows(self, y0: int, y1: int) -> np.ndarray:
+        out = np.empty((max(y1 - y0, 0), self.W), dtype=np.uint8)
+        self._check(self._L.gol_engine_store_rows(self._h, y0, y1, out.ctypes.data, self.W))
         return out
 
     def write_pgm(self, path: str) -> None:
-        check(lib().gol_engine_write_pgm(self._h, path.encode()))
+        self._check(self._L.gol_engine_write_pgm(self._h, path.encode()))
 
     # -- stepping and queries
     def step(self, turns: int) -> None:
-        check(lib().gol_engine_step(self._h, turns))
+        self._check(self._L.gol_engine_step(self._h, turns))
+
+    def step_counted(self, turns: int, every: int) -> np.ndarray:
+        """Advance `turns` turns; the alive count after every `every` turns (fused on the GPU)."""
+        n = turns // every if every > 0 else 0
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        self._check(self._L.gol_engine_step_counted(self._h, turns, every, out.ctypes.data, n))
+        return out[:n]
 
     @property
     def turn(self) -> int:
         t = ctypes.c_int64()
-        check(lib().gol_engine_turn(self._h, ctypes.byref(t)))
+        self._check(self._L.gol_engine_turn(self._h, ctypes.byref(t)))
         return t.value
 
     def alive_count(self) -> int:
         c = ctypes.c_uint64()
-        check(lib().gol_engine_alive_count(self._h, ctypes.byref(c)))
+        self._check(self._L.gol_engine_alive_count(self._h, ctypes.byref(c)))
         return c.value
 
     def alive_cells(self, cap: int | None = None) -> np.ndarray:
@@ -80,7 +130,7 @@ class Engine:
             cap = self.alive_count()
         xy = np.zeros((max(cap, 1), 2), dtype=np.int32)
         n = ctypes.c_int64()
-        check(lib().gol_engine_alive_cells(self._h, xy.ctypes.data, cap, ctypes.byref(n)))
+        self._check(self._L.gol_engine_alive_cells(self._h, xy.ctypes.data, cap, ctypes.byref(n)))
         return xy[:min(n.value, cap)]
 
     def step_flips(self, cap: int | None = None) -> np.ndarray:
@@ -90,25 +140,45 @@ class Engine:
             cap = self.H * self.W
         xy = np.zeros((max(cap, 1), 2), dtype=np.int32)
         n = ctypes.c_int64()
-        check(lib().gol_engine_step_flips(self._h, xy.ctypes.data, cap, ctypes.byref(n)))
+        self._check(self._L.gol_engine_step_flips(self._h, xy.ctypes.data, cap, ctypes.byref(n)))
         return xy[:min(n.value, cap)]
 
     def hash(self) -> int:
         h = ctypes.c_uint64()
-        check(lib().gol_engine_hash(self._h, ctypes.byref(h)))
+        self._check(self._L.gol_engine_hash(self._h, ctypes.byref(h)))
         return h.value
 
     def info(self) -> dict:
         k, cpl, strip, bm = (ctypes.c_int32() for _ in range(4))
-        check(lib().gol_engine_info(self._h, ctypes.byref(k), ctypes.byref(cpl), ctypes.byref(strip),
+        self._check(self._L.gol_engine_info(self._h, ctypes.byref(k), ctypes.byref(cpl), ctypes.byref(strip),
                                     ctypes.byref(bm)))
         return {"turns_per_launch": k.value, "cells_per_lane": cpl.value, "strip_rows": strip.value,
                 "bit_mode": bool(bm.value), "layout": {0: None, 1: "standard", 2: "band"}[bm.value]}
 
+    def topology(self) -> dict:
+        s, n, r, t = (ctypes.c_int32() for _ in range(4))
+        self._check(self._L.gol_engine_topology(self._h, ctypes.byref(s), ctypes.byref(n), ctypes.byref(r),
+                                                ctypes.byref(t)))
+        return {"shards": s.value, "nranks": n.value, "rank": r.value, "transport": TRANSPORT_NAMES[t.value]}
+
+    def shard(self, i: int) -> dict:
+        d, a, b = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._L.gol_engine_shard(self._h, i, ctypes.byref(d), ctypes.byref(a), ctypes.byref(b)))
+        return {"device": d.value, "y0": a.value, "y1": b.value}
+
+    def set_timing(self, enable: bool) -> None:
+        self._check(self._L.gol_engine_set_timing(self._h, 1 if enable else 0))
+
+    def timing(self) -> dict:
+        """HIP-event timing of the step-kernel launches since set_timing(True)."""
+        n, ms, cells = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        self._check(self._L.gol_engine_timing(self._h, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(cells)))
+        return {"launches": n.value, "mean_ms": ms.value, "mean_cell_updates": cells.value}
+
     def device_bits(self):
         p = ctypes.c_void_p()
         pitch = ctypes.c_int64()
-        check(lib().gol_engine_device_bits(self._h, ctypes.byref(p), ctypes.byref(pitch)))
+        self._check(self._L.gol_engine_device_bits(self._h, ctypes.byref(p), ctypes.byref(pitch)))
         return p.value, pitch.value
 
 

@@ -36,17 +36,18 @@
 extern "C" {
 #endif
 
-#define GOL_ABI_VERSION 1
+#define GOL_ABI_VERSION 2
 
 enum {
     GOL_OK = 0,
     GOL_EINVAL = -1,   /* bad argument */
-    GOL_EHIP = -2,     /* HIP runtime error */
+    GOL_EHIP = -2,     /* HIP runtime error, or a kernel reported a device-side fault */
     GOL_ENOMEM = -3,   /* allocation failed */
     GOL_EIO = -4,      /* file I/O */
     GOL_EFORMAT = -5,  /* malformed PGM (io.go:101-117 panics) */
     GOL_ESTATE = -6,   /* call not valid in the current state */
-    GOL_EQUIT = -7     /* broker was shut down (SuperQuit) */
+    GOL_EQUIT = -7,    /* broker was shut down (SuperQuit) */
+    GOL_ECOMM = -8     /* RCCL (halo exchange / reduction) error */
 };
 
 /* ---------------------------------------------------------------- library */
@@ -72,10 +73,26 @@ int gol_next_state_slab(const uint8_t *world, int64_t H, int64_t W, int64_t stri
 int gol_partition_rows(int64_t H, int64_t parts, int64_t i, int64_t *y0, int64_t *y1);
 
 /* ---------------------------------------------------------------- engine
- * A board resident on one GPU.  Replaces the broker's per-turn state
- * (`world`, `cWorld`, `cTurn`: broker.go:22-36, 62-234) and the per-turn
- * scatter/gather to workers (broker.go:143-157, 182-211): the board stays in
- * HBM and is stepped in k-turn launches. */
+ * A board resident in HBM, on one GPU or row-sharded over several.  Replaces
+ * the broker's per-turn state (`world`, `cWorld`, `cTurn`: broker.go:22-36,
+ * 62-234) and the per-turn scatter/gather to workers (broker.go:143-157,
+ * 182-211): the board stays in HBM and is stepped in k-turn launches.
+ *
+ * Row sharding (broker.go:135-206 applied to GPUs): the board's rows are split
+ * with gol_partition_rows over `nranks` shards; shard r keeps rows
+ * [y0_r, y1_r) plus 16 ghost rows above and below.  Before every k-turn
+ * launch each shard receives the k rows above it from shard r-1 and the k rows
+ * below it from shard r+1 (mod nranks) into its ghost rows, while the interior
+ * rows [k, R-k), which need no halo, are already being computed; the boundary
+ * rows follow once the halo is in.  k <= min shard rows.
+ *  - one process, `shards` local shards (gol_config.shards): GPUs device,
+ *    device+1, ... (or all on `device` with GOL_SHARDS_SAME_DEVICE);
+ *  - one process per GPU (gol_engine_create_rank): this process holds shard
+ *    `rank` of `nranks`; whole-board queries (alive count, hash, PGM write,
+ *    counted steps) are collective: every rank calls them.
+ * Transports of the halo rows: RCCL ncclSend/ncclRecv on a per-shard comm
+ * stream (xGMI between GPUs), or LOOPBACK device copies between the shards of
+ * one process (shards may share a GPU: multi-shard logic on a 1-GPU box). */
 typedef struct gol_engine gol_engine;
 
 /* Bit-board layout used while stepping.  STANDARD: word s of a row holds cells
@@ -86,54 +103,104 @@ typedef struct gol_engine gol_engine;
 #define GOL_LAYOUT_AUTO 0
 #define GOL_LAYOUT_STANDARD 1
 #define GOL_LAYOUT_BAND 2
+/* Halo transport between shards. */
+#define GOL_TRANSPORT_AUTO 0     /* 1 shard: local torus wrap; shards on distinct GPUs: RCCL; else LOOPBACK */
+#define GOL_TRANSPORT_LOOPBACK 1 /* device copies between the shards of this process */
+#define GOL_TRANSPORT_RCCL 2     /* ncclSend/ncclRecv (with one shard: send to self) */
+#define GOL_TRANSPORT_LOCAL 3    /* (reported only) one shard, wrap rows copied on its own stream */
+/* gol_config.flags */
+#define GOL_SHARDS_SAME_DEVICE 1 /* every local shard on `device` (loopback testing on one GPU) */
 typedef struct gol_config {
-    int32_t device;           /* HIP device ordinal; -1 = current device */
+    int32_t device;           /* HIP device ordinal (first shard); -1 = current device */
     int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
     int32_t strip_rows;       /* rows per wave strip; 0 = automatic */
     int32_t cells_per_lane;   /* 32, 64 or 128 bits per lane; 0 = automatic */
     int32_t layout;           /* bit-board layout while stepping: GOL_LAYOUT_* */
-    int32_t reserved[3];
+    int32_t shards;           /* row shards in this process (0 or 1 = one GPU, no sharding) */
+    int32_t transport;        /* GOL_TRANSPORT_* */
+    int32_t flags;            /* GOL_SHARDS_* */
 } gol_config;
 
 int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, gol_engine **out);
+/* One process per GPU: every rank calls this (collective) with the same H, W,
+ * nranks and unique id (from gol_rccl_unique_id on one rank, shared by the
+ * caller's own means, e.g. torch.distributed or the Go broker's RPC).  cfg->device
+ * is this rank's GPU.  Needs W % 64 == 0 and H >= nranks. */
+#define GOL_RCCL_ID_BYTES 128
+int gol_rccl_unique_id(uint8_t *id, int64_t len);
+int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int32_t rank, const uint8_t *id,
+                           const gol_config *cfg, gol_engine **out);
 void gol_engine_destroy(gol_engine *e);
+/* Layout of the engine: local shards, global ranks, the first local shard's
+ * global rank, and the halo transport in use (GOL_TRANSPORT_LOOPBACK, _RCCL or
+ * _LOCAL). */
+int gol_engine_topology(gol_engine *e, int32_t *shards, int32_t *nranks, int32_t *rank, int32_t *transport);
+/* Local shard i: its GPU and its global rows [y0, y1). */
+int gol_engine_shard(gol_engine *e, int32_t i, int32_t *device, int64_t *y0, int64_t *y1);
 /* Load a byte board (operations.Run's req.World, broker.go:65) and reset the
- * turn counter to 0.  Any byte value is accepted (exact semantics above). */
+ * turn counter to 0.  Any byte value is accepted (exact semantics above).
+ * `world` is the whole H x W board (as the reference ships it to every
+ * worker); every rank reads its own rows. */
 int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_t stride);
+/* Load images/<W>x<H>.pgm-style P5 (readPgmImage, gol/io.go:90-126: fields
+ * "P5", W, H, 255, then the raster): every shard streams its own rows from
+ * the file.  GOL_EFORMAT with the reference's panic text on a bad header, a
+ * short raster or (the reference's strings.Fields split) whitespace bytes in
+ * it. */
+int gol_engine_load_pgm(gol_engine *e, const char *path);
 /* Synthetic board: word(y, w) = splitmix64(seed ^ (y*W/64 + w)), Bernoulli(1/2)
  * per cell (W % 64 == 0 only).  Resets the turn counter. */
 int gol_engine_load_random(gol_engine *e, uint64_t seed);
 /* Advance exactly `turns` turns (blocking).  Replaces the turn loop body of
  * broker.go:75-226. */
 int gol_engine_step(gol_engine *e, int64_t turns);
+/* Advance exactly `turns` turns and record the alive count every `every`
+ * turns (the AliveCellsCount events of distributor.go:39-51, computed on the
+ * GPU: fused into the launch that ends at each such turn, then reduced on the
+ * device and, between ranks, with one RCCL all-reduce at the end).  counts[i]
+ * = alive cells after turn (start + (i+1)*every); writes turns/every counts
+ * (cap >= turns/every).  One host synchronisation for the whole call. */
+int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t every, uint64_t *counts, int64_t cap);
 int gol_engine_turn(gol_engine *e, int64_t *turn);
 /* Number of cells != 0 -- len(calculateAliveCells(...)), broker.go:273. */
 int gol_engine_alive_count(gol_engine *e, uint64_t *count);
-/* Copy the board out as bytes (0/255, or the loaded bytes before turn 1). */
+/* Copy the board out as bytes (0/255, or the loaded bytes before turn 1).
+ * Needs every row local (not with nranks > 1 ranks: use store_rows). */
 int gol_engine_store_bytes(gol_engine *e, uint8_t *out, int64_t stride);
+/* Rows [y0, y1) of the board (global row numbers, all held by this process). */
+int gol_engine_store_rows(gol_engine *e, int64_t y0, int64_t y1, uint8_t *out, int64_t stride);
 /* calculateAliveCells (broker.go:47-58): (x, y) int32 pairs in row-major
- * order; writes min(n, cap) pairs, *n = total alive cells. */
+ * order; writes min(n, cap) pairs, *n = total alive cells.  With ranks in
+ * several processes: the cells of this rank's rows. */
 int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n);
 /* Advance exactly one turn and list the cells whose state changed, (x, y) int32
  * pairs in row-major order: the CellFlipped{CompletedTurns, Cell} events of
  * that turn (gol/event.go:50-60; sent per flipped cell by the controller the
  * reference never finished, README.md:260-262).  Writes min(n, cap) pairs,
- * *n = number of flipped cells. */
+ * *n = number of flipped cells (of this rank's rows with several processes). */
 int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n);
 /* writePgmImage byte stream (gol/io.go:52-81): "P5\n<W> <H>\n255\n" + H*W
- * bytes, streamed from the device in chunks. */
+ * bytes, streamed from the device in chunks; with several processes every
+ * rank writes its own rows at their offset (collective). */
 int gol_engine_write_pgm(gol_engine *e, const char *path);
 /* Order-independent board hash (same definition as oracle_hash_words):
  * sum over 64-bit words of splitmix64(word ^ splitmix64(y*W/64 + w)).
  * W % 64 == 0 only. */
 int gol_engine_hash(gol_engine *e, uint64_t *hash);
 /* Chosen kernel parameters (k, cells per lane, strip rows, resident mode: 0 =
- * byte board, 1 = bit board). */
+ * byte board, 1 = standard bit board, 2 = band bit board). */
 int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lane, int32_t *strip_rows,
                     int32_t *bit_mode);
-/* Raw device pointer to the current bit board (pitch in uint32 words), for
- * tests and the PGM snapshot of a sharded board. */
+/* Raw device pointer to the current bit board of local shard 0 (pitch in
+ * uint32 words), for tests. */
 int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *pitch);
+/* Kernel timing: with timing on, HIP events on the launching stream bracket
+ * every launch of the step kernel over a shard's interior rows (or all its
+ * rows when it has no separate interior launch).  gol_engine_timing returns
+ * the number of timed launches since timing was (re)enabled, their mean
+ * duration and their mean cell-updates (rows x W x k). */
+int gol_engine_set_timing(gol_engine *e, int32_t enable);
+int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double *mean_cell_updates);
 
 /* ---------------------------------------------------------------- device launchers
  * Asynchronous kernel launches on caller-owned device memory and a caller
@@ -188,9 +255,12 @@ int gol_dev_bytes_step_k(const uint8_t *top, const uint8_t *mid, const uint8_t *
 /* k turns of a BAND-layout bit board (bit b of word w = cell b*Wd + w); row
  * addressing and count_slots as gol_dev_bits_step.  cells_per_lane: 64 or 128
  * (2 or 4 words per lane; 0 = library default); k in {1, 2, 4, 8}, 16 with 64
- * cells per lane, 12 with 128 (the split pipeline: 4 waves x 3 turns); Wd and pitch multiples of the words per lane, rows aligned
- * to 4 bytes x words per lane.  Same cells as gol_dev_bits_step on the standard
- * layout, with no bit shifts in the generation. */
+ * cells per lane, 12 with 128 (the split pipeline: 4 waves x 3 turns); Wd and
+ * pitch multiples of the words per lane, rows aligned to 4 bytes x words per
+ * lane.  Same cells as gol_dev_bits_step on the standard layout, with no bit
+ * shifts in the generation.  The pipelined kernels (k = 12 here, k = 32 in
+ * gol_dev_bytes_step_k) report a device-side protocol fault in the device's
+ * error word: check it with gol_dev_error after synchronising the stream. */
 int gol_dev_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst,
                       int64_t R, int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int32_t k,
                       int32_t cells_per_lane, int32_t strip_rows, uint64_t *count_slots, void *stream);
@@ -201,6 +271,11 @@ int gol_band_max_k(int32_t cells_per_lane);
  * != 0: standard -> band), out of place; Wd % 32 == 0 (W % 1024 == 0). */
 int gol_dev_band_convert(int32_t to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
                          int64_t src_pitch, int64_t dst_pitch, void *stream);
+/* Read and clear the error word of `device` (-1 = current) that the gol_dev_*
+ * launchers' kernels report into (*flags = 0: no fault; nonzero: a pipeline
+ * wave timed out waiting for its neighbour, so the launch's output is not
+ * valid).  Synchronous; returns GOL_EHIP when *flags != 0. */
+int gol_dev_error(int32_t device, uint32_t *flags);
 /* ---------------------------------------------------------------- RPC service mirror
  * The broker's net/rpc service `Operations` (broker.go:62-277) and the
  * worker's `GameOfLifeOperations` (worker.go:77-86) with the gob field names

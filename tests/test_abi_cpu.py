@@ -58,7 +58,7 @@ def test_header_compiles(tmp_path, compiler, lang):
 
 
 def test_abi_version(G):
-    assert G.lib().gol_abi_version() == 1
+    assert G.lib().gol_abi_version() == 2
 
 
 @pytest.mark.parametrize("H,T", [(512, 4), (512, 16), (16, 3), (64, 7), (17, 5), (10, 16), (1, 1), (0, 3)])
@@ -130,3 +130,24 @@ def test_pipe_kernels_wait_before_reading_lds(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "0 hazards" in r.stdout
+
+
+def test_go_shims_use_only_declared_c_symbols():
+    """The cgo drop-ins under go/ (not compiled here: no Go toolchain) call only functions, types
+    and constants golhip.h declares, and fill only fields of its structs."""
+    header = open(HEADER).read()
+    decl = set(declared_functions())
+    names = set(re.findall(r"\b(gol_[a-z_0-9]+|GOL_[A-Z_0-9]+)\b", header))
+    used, fields = set(), set()
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "go")):
+        for f in files:
+            if f.endswith(".go"):
+                text = open(os.path.join(dirpath, f)).read()
+                used |= set(re.findall(r"\bC\.(gol_[a-z_0-9]+|GOL_[A-Z_0-9]+)", text))
+                for lit in re.findall(r"C\.gol_(?:config|request|response)\{([^}]*)\}", text):
+                    fields |= set(re.findall(r"(\w+):", lit))
+                fields |= set(re.findall(r"\bc(?:req|res)\.(\w+)\b", text))
+    assert used and used <= (names | decl), sorted(used - names - decl)
+    struct_text = " ".join(re.findall(r"typedef struct gol_(?:config|request|response) \{(.*?)\}", header, re.S))
+    for f in fields:
+        assert re.search(r"\b%s\b" % f, struct_text), f

@@ -1,0 +1,56 @@
+"""CPU checks of bench.py's orchestration (no GPU): the self-launch of N ranks over gloo,
+the one-line JSON contract, and the roofline bookkeeping (a PMC profile measured on another
+gol_kernels.hip is never used)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_self_launch_two_ranks_dry_run():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run", "--steps", "4"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["ranks"] == 2
+    # max over ranks: rank 1 reported 2 ms, rank 0 1 ms
+    assert abs(d["ms_per_step"] - 2.0 / 4) < 1e-6
+    for key in ("metric", "value", "unit", "steps", "warmup", "higher_is_better", "scaling", "vs_baseline", "dtype",
+                "data", "config", "roofline", "cpu_baseline"):
+        assert key in d
+
+
+def test_world_size_mismatch_is_an_error():
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0 and "WORLD_SIZE=3" in p.stderr
+
+
+def test_roofline_uses_only_current_profiles(tmp_path, monkeypatch):
+    current = bench.kernel_source_hash()
+    entry = {"kernel_src": current, "bytes_per_launch": 3.5e10, "valu_insts_per_launch": 9.0e9,
+             "profile": "profiles/x"}
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "pmc_traffic.json").write_text(json.dumps({"a": entry, "b": dict(entry, kernel_src="0" * 16)}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    pmc, note = bench.load_pmc("a")
+    assert pmc is not None and note == "profiles/x"
+    r = bench.roofline("bits", 12.0, 131072 * 1048576 * 12, pmc, note)
+    assert r["bound"] == "valu"
+    assert abs(r["frac"] - 9.0e9 / 12e-3 / 1e9 / bench.VALU_PEAK_GINST) < 1e-4
+    assert abs(r["hbm"]["frac"] - 3.5e10 / 12e-3 / 1e9 / 8000) < 1e-4
+    assert abs(r["effective_GBs"] - 0.25 * 131072 * 1048576 * 12 / 12e-3 / 1e9) < 0.1
+    stale, why = bench.load_pmc("b")
+    assert stale is None and why.startswith("stale")
+    r = bench.roofline("bits", 12.0, 1e12, None, "missing")
+    assert r["bound"] == "hbm" and r["frac"] is None and r["traffic"] is None

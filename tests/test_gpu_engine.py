@@ -7,6 +7,7 @@ Mirrors the reference's end-to-end tests:
   TestAlive count_test.go:17-69   -> test_alive_counts_csv / test_alive_parity_rule
 plus size-independent properties at the bench's full size.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -434,54 +435,52 @@ def test_byte_board_k_turn_kernel(golhip, k):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("env", [{"GOL_BAND_VF": "1"}, {"GOL_SPLIT_SYNC": "0"}, {"GOL_BAND_SPLIT": "1"}])
-def test_alternative_band_kernels(golhip, env):
-    """The selectable alternatives of the band step (vertical-first one-wave kernel, barrier-
-    synchronised split pipeline, split pipeline at k = 8) against the bit oracle.  The switches
-    are read once per process, so each runs in a child process."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = (
-        "import sys; sys.path[:0] = [%r, %r]\n"
-        "import golhip\n"
-        "from oracle import oracle as O\n"
-        "for k in (8, 12):\n"
-        "    with golhip.Engine(140, 3072, device=0, turns_per_launch=k, layout='band') as e:\n"
-        "        e.load_random(31 + k)\n"
-        "        e.step(29)\n"
-        "        assert e.hash() == O.hash_words(O.bits_run(O.random_words(31 + k, 0, 140, 48), 29)), k\n"
-        "print('ok')\n" % (root, os.path.join(root, "gol-distributed-final_amd")))
-    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
-                       timeout=120)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+def _bytes_k_steps(board, k, launches, strip, splits):
+    """gol_dev_bytes_step_k on a (H, W) 0/255 torus: `launches` k-turn launches, each over the row
+    ranges `splits` (several launches per turn step); returns the board after k*launches turns."""
+    import torch
+    from golhip._lib import check, lib
+    H, W = board.shape
+    a = torch.from_numpy(board).cuda()
+    b = torch.empty_like(a)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(launches):
+        top = a[H - k:]
+        for r0, r1 in splits:
+            check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W,
+                                             r0, r1 - r0, k, strip, None, st))
+        a, b = b, a
+    torch.cuda.synchronize()
+    flags = ctypes.c_uint32()
+    check(lib().gol_dev_error(-1, ctypes.byref(flags)))
+    return a.cpu().numpy()
 
 
-def test_byte_pipe_k16_switch(golhip):
-    """GOL_BYTES_PIPE16=1 runs k = 16 on the 4-wave byte pipeline (child process: the switch is
-    read once per process); exact against the oracle with a two-launch row split."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = (
-        "import sys; sys.path[:0] = [%r, %r]\n"
-        "import numpy as np, torch\n"
-        "from golhip._lib import check, lib\n"
-        "from oracle import oracle as O\n"
-        "H, W, k = 150, 32 * 40, 16\n"
-        "board = (np.random.default_rng(3).random((H, W)) < 0.4).astype(np.uint8) * 255\n"
-        "a = torch.from_numpy(board).cuda(); b = torch.empty_like(a)\n"
-        "st = torch.cuda.current_stream().cuda_stream\n"
-        "for _ in range(2):\n"
-        "    top = a[H - k:]\n"
-        "    check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W, 0, 70, k, 0, None, st))\n"
-        "    check(lib().gol_dev_bytes_step_k(top.data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W, W, 70, H - 70, k, 0, None, st))\n"
-        "    a, b = b, a\n"
-        "assert np.array_equal(a.cpu().numpy(), O.run(board, 2 * k))\n"
-        "print('ok')\n" % (root, os.path.join(root, "gol-distributed-final_amd")))
-    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "GOL_BYTES_PIPE16": "1"},
-                       capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+@pytest.mark.parametrize("H,strip", [(620, 130), (1100, 0), (700, 64)])
+def test_byte_pipe_several_strips(golhip, H, strip):
+    """The k = 32 byte pipeline (8 waves x 4 turns) with several strips per launch (blockIdx.y > 0):
+    explicit 130- and 64-row strips and the automatic round-tiled strip at >= 1024 rows, against
+    the bit oracle; the second launch splits the rows in two ranges (strip edges inside a launch)."""
+    W = 32 * 96
+    rng = np.random.default_rng(H + strip)
+    board = (rng.random((H, W)) < 0.4).astype(np.uint8) * 255
+    got = _bytes_k_steps(board, 32, 2, strip, [(0, H)])
+    ref = O.unpack(O.bits_run(O.pack(board), 64))
+    assert np.array_equal(got, ref)
+    got2 = _bytes_k_steps(board, 32, 1, strip, [(0, 333), (333, H)])
+    assert np.array_equal(got2, O.unpack(O.bits_run(O.pack(board), 32)))
+
+
+def test_byte16k_full_size_parity(golhip):
+    """Config 2 at its size: the 16384 x 16384 byte board, two k = 32 launches (the bench's
+    kernel, automatic strips: many strips per column group) against the bit oracle's 64 turns."""
+    H = W = 16384
+    words = O.random_words(1, 0, H, W // 64)
+    board = O.unpack(words)
+    got = _bytes_k_steps(board, 32, 2, 0, [(0, H)])
+    ref = O.bits_run(words, 64)
+    assert O.hash_words(O.pack(got)) == O.hash_words(ref)
+    assert np.array_equal(got, O.unpack(ref))
 
 
 # ------------------------------------------------------------------ CellFlipped stream

@@ -134,35 +134,34 @@ def test_sharded_gpu_load_pgm_band(tmp_path):
     assert np.array_equal(res[0][1], ref)
 
 
-def _bench_line(args, nproc, port):
-    """Run bench.py (1 rank, or `nproc` ranks under torch.distributed.run) and parse its JSON line."""
+def _bench_line(args):
+    """Run bench.py (it starts its own ranks for --gpus N > 1) and parse its JSON line."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    if nproc == 1:
-        cmd = [sys.executable, "bench.py"] + args
-    else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py",
-               "--gpus", str(nproc), "--backend", "gloo", "--share-gpu"] + args
-    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=150)
+    p = subprocess.run([sys.executable, "bench.py"] + args, cwd=root, capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     return json.loads(lines[0])
 
 
-def test_bench_two_ranks_match_one_rank():
-    """bench.py's N > 1 path (barrier, max-over-ranks timing, sharded weak board, fused count):
-    2 ranks x 2048 rows give the same alive count as 1 rank x 4096 rows of the same torus
-    (the synthetic board is a function of the global row), and the line reports the whole job."""
-    common = ["--width", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
-    two = _bench_line(["--rows-per-gpu", "2048"] + common, 2, _free_port())
-    one = _bench_line(["--rows-per-gpu", "4096"] + common, 1, 0)
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher: the parent starts 2 ranks before touching the
+    GPU; with --share-gpu (RCCL refuses two ranks on one GPU) each rank steps its own replica of
+    the rows_per_gpu-row torus, so the line must report 2x the one-rank alive count and the
+    whole-job rate from the max-over-ranks time."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    common = ["--rows-per-gpu", "2048", "--width", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    two = _bench_line(["--gpus", "2", "--share-gpu"] + common)
+    one = _bench_line(common)
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
-    assert two["config"]["H"] == one["config"]["H"] == 4096
+    assert two["config"]["parallelism"] == "replicas2"
     assert two["config"]["turns_done"] == one["config"]["turns_done"]
-    assert two["config"]["alive_final"] == one["config"]["alive_final"]
+    assert two["config"]["alive_final"] == 2 * one["config"]["alive_final"]
     k = one["config"]["turns_per_step"]
-    assert abs(two["value"] - 4096 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
+    assert abs(two["value"] - 2 * 2048 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
+    assert one["roofline"]["launch_ms"] > 0 and one["config"]["timed_launches"] == 3

@@ -119,6 +119,14 @@ def main():
         for i, s, r in check(body):
             bad += 1
             print(f"{name}: line {i}: reads in-flight v{r}: {s}")
+    # the pipeline kernels must not spill: scratch traffic inside the pipeline loop costs more
+    # than the kernel's whole LDS hand-off (and reads in-flight registers, as above)
+    for blk in re.findall(r"- \.agpr_count.*?(?=\n  - \.agpr_count|\namdhsa\.target)", asm, re.S):
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        scratch = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+        if re.search(args.pattern, name) and scratch and int(scratch.group(1)):
+            bad += 1
+            print(f"{name}: {scratch.group(1)} bytes of scratch (register spills)")
     print(f"{n} kernels checked, {bad} hazards")
     return 1 if bad or n == 0 else 0
 

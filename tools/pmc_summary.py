@@ -1,12 +1,17 @@
 """Summarise a tools/profile.sh run into profiles/<tag>/ (tracked):
   kernel_stats.csv       rocprofv3 --stats summary of the bench command
   pmc_summary.json       per-kernel means of the PMC passes + derived HBM bytes, clock, VALU use
-and update profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+and update profiles/pmc_traffic.json, read by bench.py for the roofline (HBM bytes and wave64
+VALU instructions per launch of the step kernel).  Each entry records the sha256 prefix of the
+gol_kernels.hip it was measured on; bench.py ignores an entry whose hash differs.
+
+    python tools/pmc_summary.py <tag> <bench key, e.g. weak:131072x1048576:k12:band>
 
 HBM bytes per launch = FETCH_SIZE*2 + WRITE_SIZE (KiB -> bytes), the gfx950 correction of
 MI355X_MICROARCH.md §HBM (FETCH_SIZE reports half of a wide streaming read)."""
 import collections
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -52,9 +57,19 @@ if not out:
 main = max(out, key=lambda k: out[k].get("avg_ns_trace") or 0)
 tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 t = json.load(open(tp)) if os.path.exists(tp) else {}
+src_hash = hashlib.sha256(open(os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernels.hip"),
+                                "rb").read()).hexdigest()[:16]
 if "hbm_bytes_per_launch" in out[main]:
-    t[key] = {"kernel": main, "bytes_per_launch": out[main]["hbm_bytes_per_launch"], "profile": f"profiles/{tag}"}
+    t[key] = {"kernel": main, "kernel_src": src_hash, "bytes_per_launch": out[main]["hbm_bytes_per_launch"],
+              "profile": f"profiles/{tag}", "avg_ns_trace": out[main]["avg_ns_trace"]}
+    c = out[main]["counters"]
+    if "SQ_INSTS_VALU" in c:
+        t[key]["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+    if "SQ_INSTS_SALU" in c:
+        t[key]["salu_insts_per_launch"] = c["SQ_INSTS_SALU"]
     if "valu_issue_frac" in out[main]:
-        t[key]["valu_issue_frac"] = round(out[main]["valu_issue_frac"], 4)
+        t[key]["valu_issue_frac_profile_clock"] = round(out[main]["valu_issue_frac"], 4)
+    if "clock_GHz" in out[main]:
+        t[key]["clock_GHz"] = round(out[main]["clock_GHz"], 3)
     json.dump(t, open(tp, "w"), indent=1)
 print(json.dumps(out[main], indent=1))
