@@ -185,6 +185,18 @@ __device__ __forceinline__ void sstage(Pipe<K, DW> &p, const int g, uint32_t (&c
                       p.h1[g][S][j], p.cc[g][SM][j]);
 }
 
+// Work items of the pipelined kernels (one workgroup = one column group x one strip of rows).
+// ranked = 0: equal strips of `strip` rows, workgroup l -> XCD-remapped item.  ranked = 1 (a
+// launch of exactly one round, cus x per_cu workgroups): the dispatcher deals workgroup l to CU
+// l % cus as the (l / cus)-th arrival there, and a SIMD issues to its oldest ready wave first,
+// so the CU's workgroups run at different speeds (one round of equal strips ended them at 247 /
+// 298 / 388 / 482 us, tools/timeline.py); each CU then takes one column group x `period` rows
+// and splits the rows by arrival rank: rank r gets len[r] rows at off[r].
+struct StripMap {
+    int32_t ranked, cus, per_cu, period;
+    int32_t len[4], off[4];
+};
+
 struct BitsArgs {
     const uint32_t *top, *mid, *bot;
     uint32_t *dst;
@@ -192,7 +204,37 @@ struct BitsArgs {
     int32_t strip, ngroups;
     uint64_t *slots;
     uint32_t *err;
+    StripMap sm;
 };
+
+// Column group, strip [s0, s1) and a per-CU rotation index of workgroup l (1-D grid); false:
+// the workgroup has no rows.
+__device__ __forceinline__ bool work_item(const StripMap &sm, int ngroups, int64_t row0, int64_t rows, int strip, int l,
+                                          int &group, int &s0, int &s1, int &rot)
+{
+    const int end = (int)(row0 + rows);
+    if (!sm.ranked) {
+        // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (L2 per XCD), so
+        // consecutive ids are remapped to let each XCD walk its own contiguous run of column groups
+        // of a strip: the lateral halo columns two neighbouring groups both read then meet in one L2.
+        const int n = gridDim.x, per = n / 8;
+        const int m = l < per * 8 ? (l % 8) * per + l / 8 : l;
+        group = m % ngroups;
+        const int by = m / ngroups;
+        s0 = (int)row0 + by * strip;
+        s1 = min(s0 + strip, end);
+        rot = group + by;
+    } else {
+        const int rank = l / sm.cus, c = l % sm.cus;
+        const int c2 = (c % 8) * (sm.cus / 8) + c / 8;  // contiguous CUs per XCD (cus % 8 == 0)
+        group = c2 % ngroups;
+        const int t = c2 / ngroups;
+        s0 = (int)row0 + t * sm.period + sm.off[rank];
+        s1 = min(s0 + sm.len[rank], end);
+        rot = rank;
+    }
+    return s0 < s1;
+}
 
 // ------------------------------------------------------------------ bit-board step, standard layout
 // grid.x: groups of 4 waves along the row; grid.y: strips of output rows.
@@ -560,7 +602,8 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 // waves per SIMD.  Wave 0 stages its input rows HBM -> LDS with global_load_lds (no VGPRs),
 // wave P-1 stores to HBM.  Synchronisation is per ring, by LDS flags: ready[e] = blocks
 // published into ring e, consumed[e] = blocks taken out of it; a producer fills slot b % 3
-// once block b-3 is consumed.  Every spin is bounded (spin_until_ge).
+// once block b-3 is consumed.  Every spin is bounded (spin_until_ge).  1-D grid of work items
+// (work_item).
 template <int KW, int P, bool CONTIG>
 __global__ void __launch_bounds__(64 * P)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
@@ -578,35 +621,21 @@ band_pipe_kernel(BitsArgs a)
     __shared__ int flag_scratch[P][64];
 
     const int lane = threadIdx.x & 63;
-    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (L2 per XCD), so
-    // consecutive ids are remapped to let each XCD walk its own contiguous run of column groups
-    // of a strip: the lateral halo columns two neighbouring groups both read then meet in one L2.
-    int bx = blockIdx.x, by = blockIdx.y;
-    {
-        const int n = gridDim.x * gridDim.y, l = blockIdx.x + blockIdx.y * gridDim.x;
-        const int per = n / 8;
-        if (l < per * 8) {
-            const int m = (l % 8) * per + l / 8;
-            bx = m % gridDim.x;
-            by = m / gridDim.x;
-        }
-    }
-    // Pipeline position of this wave, rotated by workgroup: the waves of a workgroup sit on
-    // the CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put
-    // its loader (global_load_lds) on one SIMD and its storer on another.
-    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + (bx + by)) % P);
-    const int group = bx;
+    int group, s0, s1, rotv;
+    const bool has_rows = work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv);
+    // Pipeline position of this wave, rotated per workgroup: the waves of a workgroup sit on the
+    // CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put its
+    // loader (global_load_lds) on one SIMD and its storer on another.
+    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
-    const int64_t q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
-    const int64_t col = col_raw - q * a.Wd;
-    const uint32_t rot = (uint32_t)q & 31u;
+    const int64_t band_q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
+    const int64_t col = col_raw - band_q * a.Wd;
+    const uint32_t rot = (uint32_t)band_q & 31u;
     const bool wrap = __ballot(rot != 0) != 0;
     const bool writer = lane >= HL && lane < 64 - HL && col_raw < a.Wd;
 
     const int R = (int)a.R;
-    const int s0 = (int)a.row0 + by * a.strip;
-    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
     const int first_in = s0 - K;
     const int last_in = s1 + K - 1;
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
@@ -632,6 +661,7 @@ band_pipe_kernel(BitsArgs a)
         }
     };
 
+    if (!has_rows) return;  // whole workgroup (no barrier after this point)
     if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
     __syncthreads();
     lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
@@ -883,6 +913,7 @@ struct BytesKArgs {
     int32_t strip, ngroups;
     uint64_t *slots;
     uint32_t *err;
+    StripMap sm;
 };
 
 // Byte rows of one lane: 32 bytes = two 16-byte loads, packed to a word at use.
@@ -991,6 +1022,7 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
         : "memory");
 }
 
+// 1-D grid of work items (work_item).
 template <int KW, int P>
 __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 {
@@ -1003,13 +1035,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int group = blockIdx.x;
+    int group, s0, s1, rotv;
+    if (!work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv)) return;
     const int64_t col_raw = (int64_t)group * 62 + (lane - 1);
     const int64_t col = ((col_raw % a.Wd) + a.Wd) % a.Wd;
     const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
     const int R = (int)a.R;
-    const int s0 = (int)a.row0 + (int)blockIdx.y * a.strip;
-    const int s1 = min(s0 + a.strip, (int)(a.row0 + a.rows));
     const int first_in = s0 - K, last_in = s1 + K - 1;
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
     const int pitch = (int)a.pitch;
@@ -1576,6 +1607,7 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.ngroups = (int)((Wd + 62 * dw - 1) / (62 * dw));
     a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
     a.slots = slots;
+    a.sm = StripMap{};
     a.err = nullptr;  // no flag waits in this kernel
     if (rows <= 0) return hipSuccess;
     switch (dw) {
@@ -1601,19 +1633,82 @@ static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s
     return hipGetLastError();
 }
 
+static int device_cus()
+{
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return cus;
+}
+
+// Rank-weighted strips for a launch of exactly one round (StripMap): every CU takes one column
+// group x `period` rows and its per_cu workgroups split them in proportion to `weight[rank]`,
+// the measured relative speed of the rank-th arrival on a CU.  Used when the strips of one
+// column group can be spread over the CUs with little waste (ngroups x strips per group >= 94 %
+// of the CUs) and every rank still gets >= min_rows rows; else false (equal strips).
+static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const double *weight, int64_t min_rows,
+                       int64_t max_strip, StripMap &sm)
+{
+    if (cus <= 0 || cus % 8 || per_cu < 1 || per_cu > 4 || ngroups > cus || rows <= 0) return false;
+    // only boards that fill the device at most twice with strips of max_strip rows: on bigger
+    // boards workgroups refill the CUs as they finish, and only the last round has the tail
+    if (ngroups * ((rows + max_strip - 1) / max_strip) > 2 * (int64_t)cus * per_cu) return false;
+    const int64_t t = cus / ngroups;  // strips per column group, one CU each
+    if (t * ngroups * 100 < (int64_t)cus * 94) return false;
+    const int64_t period = (rows + t - 1) / t;
+    double wsum = 0;
+    for (int r = 0; r < per_cu; ++r) wsum += weight[r];
+    StripMap m{};
+    m.ranked = 1;
+    m.cus = cus;
+    m.per_cu = per_cu;
+    m.period = (int32_t)period;
+    int64_t off = 0;
+    for (int r = 0; r < per_cu; ++r) {
+        const int64_t len = r == per_cu - 1 ? period - off : (int64_t)(period * weight[r] / wsum + 0.5);
+        if (len < min_rows) return false;
+        m.len[r] = (int32_t)len;
+        m.off[r] = (int32_t)off;
+        off += len;
+    }
+    sm = m;
+    return true;
+}
+
+// Rows per arrival rank, from measurements (tools/timeline.py, same-box A/B with tools/ab.py):
+// one round of equal strips ended the ranks' workgroups at T_r (band 247 / 298 / 388 / 482 us,
+// bytes 96 / 136 / 174 us), so the first split gave rank r a share ~ 1 / T_r; re-measuring moved
+// rows from the late ranks to the early ones (w_r <- w_r T_mean / T_r).  65536^2 bits: 103.4 ->
+// 106.1 TCUPS; 16384^2 bytes: 43.9 -> 45.2.  (The ends of one rank still spread over ~40 us from
+// CU to CU, which a static split cannot absorb.)
+#ifndef GOL_BAND_RANK_W
+#define GOL_BAND_RANK_W 0.42, 0.28, 0.18, 0.12
+#endif
+#ifndef GOL_BYTES_RANK_W
+#define GOL_BYTES_RANK_W 0.4457, 0.3094, 0.2449, 0.0
+#endif
+static const double BAND_PIPE_RANK_W[4] = {GOL_BAND_RANK_W};
+static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
+
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
     constexpr int KW = 3, P = 4;
-    if (auto_strip) {
-        const void *kf = contig ? (const void *)band_pipe_kernel<KW, P, true> : (const void *)band_pipe_kernel<KW, P, false>;
-        a.strip = (int)round_tiled_strip(a.rows, a.ngroups, resident_workgroups(kf, 64 * P), 8 * KW * P, 1024, a.strip);
+    const void *kf = contig ? (const void *)band_pipe_kernel<KW, P, true> : (const void *)band_pipe_kernel<KW, P, false>;
+    int64_t nwg = 0;
+    const int cus = device_cus();
+    const int64_t slots = resident_workgroups(kf, 64 * P);
+    if (auto_strip && cus > 0 &&
+        rank_split(a.rows, a.ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, a.sm)) {
+        nwg = (int64_t)cus * a.sm.per_cu;
+    } else {
+        if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
+        nwg = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
     }
-    const dim3 grid(a.ngroups, (int)((a.rows + a.strip - 1) / a.strip));
     if (contig)
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), grid, dim3(64 * P), 0, s, a);
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
     else
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false>), grid, dim3(64 * P), 0, s, a);
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1626,6 +1721,7 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.top = top; a.mid = mid; a.bot = bot; a.dst = dst;
     a.R = R; a.Wd = Wd; a.pitch = pitch; a.row0 = row0; a.rows = rows;
     a.slots = slots;
+    a.sm = StripMap{};
     a.err = err_or_default(err);
     if (!a.err) return hipErrorOutOfMemory;
     const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
@@ -1700,15 +1796,25 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
     a.err = err_or_default(err);
     if (rows <= 0) return hipSuccess;
     if (!a.err) return hipErrorOutOfMemory;
+    a.sm = StripMap{};
     if (k == 32) {
-        // one workgroup of 8 waves per (column group, strip), round-tiled strips >= 4k rows
-        if (strip <= 0) {
-            a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
-            a.strip = (int)round_tiled_strip(rows, a.ngroups, resident_workgroups((const void *)bytes_pipe_kernel<4, 8>, 512),
-                                             4 * k, 1024, a.strip);
+        // one workgroup of 8 waves x 4 turns per (column group, strip): rank-weighted strips in
+        // one round, else round-tiled strips >= 4k rows
+        const void *kf = (const void *)bytes_pipe_kernel<4, 8>;
+        const int cus = device_cus();
+        const int64_t slots = resident_workgroups(kf, 512);
+        int64_t nwg = 0;
+        if (strip <= 0 && cus > 0 &&
+            rank_split(rows, a.ngroups, cus, (int)(slots / cus), BYTES_PIPE_RANK_W, 4 * k, 1024, a.sm)) {
+            nwg = (int64_t)cus * a.sm.per_cu;
+        } else {
+            if (strip <= 0) {
+                a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
+                a.strip = (int)round_tiled_strip(rows, a.ngroups, slots, 4 * k, 1024, a.strip);
+            }
+            nwg = (int64_t)a.ngroups * ((rows + a.strip - 1) / a.strip);
         }
-        const dim3 g2(a.ngroups, (int)((rows + a.strip - 1) / a.strip));
-        hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), g2, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), dim3((unsigned)nwg), dim3(512), 0, s, a);
         return hipGetLastError();
     }
     const int nstrips = (int)((rows + a.strip - 1) / a.strip);

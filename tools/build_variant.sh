@@ -1,10 +1,14 @@
 #!/bin/bash
 # Build a library variant for same-box A/B runs: tools/build_variant.sh NAME "-DFLAG=1 ..."
-# -> build_exp/libNAME.so, from a copy of the current sources with its own object dir.
+# -> tools/variants/libNAME.so, from a copy of the current sources with its own object dir.
+# (The product library has one compiled path; variants exist only as these measurement builds.)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 N=$1; F=$2
-rm -rf "$R/build_exp/src_$N" && mkdir -p "$R/build_exp/src_$N"
-cp "$R"/gol-distributed-final_amd/csrc/{Makefile,*.cpp,*.h,*.hip} "$R/build_exp/src_$N/"
-make -s -j8 -C "$R/build_exp/src_$N" ARCH=gfx950 BUILD=./obj OUT=../lib$N.so \
+D=$R/tools/variants/src_$N
+rm -rf "$D" && mkdir -p "$D"
+cp "$R"/gol-distributed-final_amd/csrc/{Makefile,*.cpp,*.h,*.hip} "$D/"
+make -s -j8 -C "$D" ARCH=gfx950 BUILD=./obj OUT=../lib$N.so INC=$R/include \
     CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -I$R/include -I. $F"
+rm -rf "$D/obj"
+echo "$R/tools/variants/lib$N.so"

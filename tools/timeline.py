@@ -1,0 +1,134 @@
+"""Per-workgroup timeline of the pipeline kernels (measurement only).
+
+Builds a copy of libgolhip.so whose band_pipe_kernel / bytes_pipe_kernel write, per wave, the
+s_memrealtime stamps (100 MHz, chip-wide) of kernel entry and exit plus the HW_ID / XCC_ID
+registers into the count-slot buffer (which the launch is given instead of count slots), runs
+one launch of a workload and summarises when workgroups start and end: how much of the kernel
+span the waves are resident, the dispatch ramp, and the tail.
+
+    python tools/timeline.py build [-DFLAG=..]     # here (hipcc), -> tools/tl/libtimeline.so
+    python tools/timeline.py run bit64k|byte16k|weak [--strip N]   # on the GPU box
+"""
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
+OUT = os.path.join(ROOT, "tools", "tl")
+LIB = os.path.join(ROOT, "tools", "tl", "libtimeline.so")
+
+ENTRY = "    const int lane = threadIdx.x & 63;\n"
+STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n"
+EXIT_BAND = "    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
+EXIT_BYTES = "    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);\n    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
+STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear workgroup id * P + wave
+        const uint64_t tl_t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        const uint64_t i = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0) {
+            a.slots[4 * i] = tl_t0; a.slots[4 * i + 1] = tl_t1;
+            a.slots[4 * i + 2] = hw; a.slots[4 * i + 3] = xcc;
+        }
+        (void)alive;
+    }
+}"""
+
+
+def build(flags=""):
+    os.makedirs(OUT, exist_ok=True)
+    src = open(os.path.join(CSRC, "gol_kernels.hip")).read()
+    for kern, exit_ in (("band_pipe_kernel(BitsArgs a)", EXIT_BAND), ("bytes_pipe_kernel(BytesKArgs a)", EXIT_BYTES)):
+        i = src.index(kern)
+        j = src.index(ENTRY, i)
+        src = src[:j] + STAMP_T0 + src[j + len(ENTRY):]
+        k = src.index(exit_, j)
+        src = src[:k] + exit_.replace("    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}", STORE) + src[k + len(exit_):]
+    open(os.path.join(OUT, "gol_kernels.hip"), "w").write(src)
+    for f in os.listdir(CSRC):
+        if f.endswith((".cpp", ".h")) or f == "Makefile":
+            with open(os.path.join(CSRC, f)) as a, open(os.path.join(OUT, f), "w") as b:
+                b.write(a.read())
+    subprocess.run(["make", "-s", "-j8", "-C", OUT, "ARCH=gfx950", "BUILD=./obj", "OUT=./libtimeline.so",
+                    f"CXXFLAGS=-O3 -std=c++17 -fPIC -Wall -I{ROOT}/include -I. {flags}", f"INC={ROOT}/include"], check=True)
+    print(LIB)
+
+
+def run(workload, strip):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gol-distributed-final_amd")]
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import golhip._lib as L
+    lib = L.load(LIB)
+    st = torch.cuda.current_stream().cuda_stream
+    if workload == "byte16k":
+        H = W = 16384
+        k, P = 32, 8
+        a = torch.zeros((H, W), dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        ngroups = (W // 32 + 61) // 62
+        buf = torch.zeros(4 * P * ngroups * H, dtype=torch.int64, device="cuda")  # generous
+        launch = lambda: lib.gol_dev_bytes_step_k(a[H - k:].data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W,  # noqa: E731
+                                                  W, 0, H, k, strip, buf.data_ptr(), st)
+    else:
+        H, W = {"bit64k": (65536, 65536), "weak": (1 << 17, 1 << 20)}[workload]
+        k, P = 12, 16  # buffer sized for up to 16 waves per work item
+        Wd = W // 32
+        g = 16
+        a = torch.zeros((H + 2 * g, Wd), dtype=torch.int32, device="cuda")
+        b = torch.zeros_like(a)
+        mid = a[g:g + H]
+        ngroups = (Wd + 231) // 232
+        buf = torch.zeros(4 * P * ngroups * H, dtype=torch.int64, device="cuda")
+        launch = lambda: lib.gol_dev_band_step(a[g - k:].data_ptr(), mid.data_ptr(), a[g + H:].data_ptr(),  # noqa: E731
+                                               b[g:].data_ptr(), H, Wd, Wd, 0, H, k, 128, strip, buf.data_ptr(), st)
+    for _ in range(3):
+        assert launch() == 0
+    torch.cuda.synchronize()
+    buf.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    assert launch() == 0
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    v = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+    v = v[v[:, 1] > 0]
+    t0, t1 = v[:, 0], v[:, 1]
+    base = t0.min()
+    s, e = (t0 - base) / 100.0, (t1 - base) / 100.0  # microseconds (100 MHz)
+    span = e.max()
+    hw, xcc = v[:, 2], v[:, 3]
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    simd = (hw >> 4) & 0x3
+    key = xcc * 1000 + se * 100 + cu
+    per_cu = {}
+    for kk in np.unique(key):
+        m = key == kk
+        per_cu[int(kk)] = (int(m.sum()), float(e[m].max()))
+    life = e - s
+    out = {"workload": workload, "strip": strip, "event_ms": round(ms, 4), "waves": int(len(v)), "span_us": round(float(span), 1),
+           "resident_frac": round(float(life.sum() / (span * 16 * 256)), 3),
+           "start_us_pct": [round(float(np.percentile(s, q)), 1) for q in (0, 10, 50, 90, 99, 100)],
+           "end_us_pct": [round(float(np.percentile(e, q)), 1) for q in (0, 1, 10, 50, 90, 100)],
+           "life_us_pct": [round(float(np.percentile(life, q)), 1) for q in (0, 10, 50, 90, 100)],
+           "cus_used": len(per_cu), "waves_per_cu": sorted({c for c, _ in per_cu.values()}),
+           "cu_end_us_pct": [round(float(np.percentile([x for _, x in per_cu.values()], q)), 1) for q in (0, 10, 50, 90, 100)],
+           "simd_hist": np.bincount(simd, minlength=4).tolist()}
+    print(json.dumps(out))
+    np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{workload}_{strip}.npy"), v)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(" ".join(sys.argv[2:]))  # extra compiler flags, e.g. -DGOL_PIPE_Q=1
+    else:
+        strip = int(sys.argv[sys.argv.index("--strip") + 1]) if "--strip" in sys.argv else 0
+        run(sys.argv[2], strip)
