@@ -37,7 +37,17 @@ def pgm_header(head: bytes, width: int | None = None, height: int | None = None)
         raise GolError(GOL_EFORMAT, "Incorrect height")
     if maxval != 255:
         raise GolError(GOL_EFORMAT, "Incorrect maxval/bit depth")
-    return W, H, i + 1  # one whitespace byte separates maxval from the raster
+    while i < n and head[i] in _SPACE:  # the raster is fields[4]: it starts at the next non-space byte
+        i += 1
+    return W, H, i
+
+
+def _check_raster(raster: np.ndarray) -> None:
+    """The reference takes the raster as strings.Fields(data)[4] (io.go:98-119): a whitespace byte
+    inside it would end the field early (and the reference would then wait for the missing
+    pixels), so such files are rejected here instead of read differently."""
+    if np.isin(raster, np.frombuffer(_SPACE, dtype=np.uint8)).any():
+        raise GolError(GOL_EFORMAT, "pixel data shorter than W*H (a whitespace byte ends the field)")
 
 
 def read_pgm(path: str, width: int | None = None, height: int | None = None) -> np.ndarray:
@@ -47,7 +57,9 @@ def read_pgm(path: str, width: int | None = None, height: int | None = None) -> 
     W, H, off = pgm_header(data[:4096], width, height)
     if len(data) < off + W * H:
         raise GolError(GOL_EFORMAT, "pixel data shorter than W*H")
-    return np.frombuffer(data, dtype=np.uint8, count=W * H, offset=off).reshape(H, W).copy()
+    raster = np.frombuffer(data, dtype=np.uint8, count=W * H, offset=off).reshape(H, W).copy()
+    _check_raster(raster)
+    return raster
 
 
 def pgm_rows(path: str, y0: int, y1: int, width: int | None = None, height: int | None = None):

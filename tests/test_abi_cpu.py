@@ -101,6 +101,14 @@ def test_pgm_reader_matches_oracle_and_errors(G, golden_dir, tmp_path):
     p = os.path.join(golden_dir, "images", "16x16.pgm")
     with pytest.raises(G.GolError, match="Incorrect width"):
         G.read_pgm(p, width=17)
+    # io.go takes the raster as strings.Fields(data)[4]: any whitespace after maxval is skipped,
+    # and a whitespace byte inside the raster would end the field (rejected)
+    good = tmp_path / "crlf.pgm"
+    good.write_bytes(b"P5\n2 2\n255\r\n\xff\x00\x00\xff")
+    assert G.read_pgm(str(good)).tolist() == [[255, 0], [0, 255]]
+    bad.write_bytes(b"P5\n2 2\n255\n\xff\x20\x00\xff")
+    with pytest.raises(G.GolError, match="whitespace"):
+        G.read_pgm(str(bad))
 
 
 def test_stub_names_match_reference(G):

@@ -145,6 +145,28 @@ def test_shards_load_pgm(G, golden_dir):
         assert np.array_equal(e.store_bytes(), board)
 
 
+def test_load_pgm_fields_rules(G, tmp_path):
+    """io.go:98-119 (strings.Fields): whitespace after maxval is skipped; a raster holding a
+    whitespace byte is rejected; bytes other than 0/255 get the exact first turn."""
+    rng = np.random.default_rng(4)
+    H, W = 40, 128
+    board = rng.choice(np.array([0, 255, 7], dtype=np.uint8), size=(H, W), p=[.5, .4, .1])
+    p = tmp_path / "b.pgm"
+    p.write_bytes(b"P5\n%d %d\n255\r\n" % (W, H) + board.tobytes())
+    for n in (1, 2):
+        with _sharded(G, H, W, n) as e:
+            e.load_pgm(str(p))
+            assert np.array_equal(e.store_bytes(), board)
+            e.step(3)
+            assert np.array_equal(e.store_bytes(), O.run(board, 3))
+    ws = board.copy()
+    ws[20, 5] = 32
+    p.write_bytes(b"P5\n%d %d\n255\n" % (W, H) + ws.tobytes())
+    with _sharded(G, H, W, 2) as e:
+        with pytest.raises(G.GolError, match="whitespace"):
+            e.load_pgm(str(p))
+
+
 def test_rccl_transport_self(G):
     """The RCCL halo path on one GPU: one shard whose ncclSend/ncclRecv go to itself (the torus
     wrap), in-process (ncclCommInitAll) and as a one-rank Engine.rank (ncclCommInitRank)."""
