@@ -24,6 +24,7 @@
 #include <map>
 #include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "gol_kernels.h"
 
@@ -183,6 +184,48 @@ __device__ __forceinline__ void sstage(Pipe<K, DW> &p, const int g, uint32_t (&c
     for (int j = 0; j < DW; ++j)
         cur[j] = rule(p.h0[g][SA][j], p.h1[g][SA][j], p.h0[g][SM][j], p.h1[g][SM][j], p.h0[g][S][j],
                       p.h1[g][S][j], p.cc[g][SM][j]);
+}
+
+// Step W of a 3-row wavefront over K shifted-frame stages, one word per lane: row r (ring slot
+// r) is at stage W - r.  The three rows' stages are independent within a step, and each op is
+// written for all active rows before the next (a one-word stage is a dependent chain of 13
+// ops; row after row, the compiler kept the chains apart and one wave issued at the
+// dependent-op latency).
+template <int K, int NSTG, int W>
+__device__ __forceinline__ void sstage_wave3(Pipe<K, 1> &p, uint32_t (&c)[3])
+{
+    static_assert(NSTG <= K, "stages of the pipe state");
+    constexpr bool on[3] = {W < NSTG, W >= 1 && W - 1 < NSTG, W >= 2 && W - 2 < NSTG};
+    constexpr int g[3] = {on[0] ? W : 0, on[1] ? W - 1 : 0, on[2] ? W - 2 : 0};
+    uint32_t wl[3], L1[3], L2[3], t0[3], k0[3], u[3], v[3], e1[3], e2[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) if (on[r]) wl[r] = from_lower_lane(c[r]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) if (on[r]) L1[r] = __builtin_amdgcn_alignbit(c[r], wl[r], 31);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) if (on[r]) L2[r] = __builtin_amdgcn_alignbit(c[r], wl[r], 30);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) if (on[r]) p.h0[g[r]][r][0] = bitop3<TT_XOR3>(L1[r], c[r], L2[r]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) if (on[r]) p.h1[g[r]][r][0] = bitop3<TT_MAJ>(L1[r], c[r], L2[r]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) if (on[r]) p.cc[g[r]][r][0] = L1[r];
+#define GOL_ROWS3(expr) _Pragma("unroll") for (int r = 0; r < 3; ++r) if (on[r]) { const int A = (r + 1) % 3, M = (r + 2) % 3; (void)A; (void)M; expr; }
+    GOL_ROWS3(k0[r] = bitop3<TT_MAJ>(p.h0[g[r]][A][0], p.h0[g[r]][M][0], p.h0[g[r]][r][0]))
+    GOL_ROWS3(u[r] = bitop3<TT_XOR3>(p.h1[g[r]][A][0], p.h1[g[r]][M][0], p.h1[g[r]][r][0]))
+    GOL_ROWS3(v[r] = bitop3<TT_MAJ>(p.h1[g[r]][A][0], p.h1[g[r]][M][0], p.h1[g[r]][r][0]))
+    GOL_ROWS3(t0[r] = bitop3<TT_XOR3>(p.h0[g[r]][A][0], p.h0[g[r]][M][0], p.h0[g[r]][r][0]))
+    GOL_ROWS3(e2[r] = bitop3<TT_EQ2>(u[r], k0[r], v[r]))
+    GOL_ROWS3(e1[r] = bitop3<TT_EQ1>(u[r], k0[r], v[r]))
+    GOL_ROWS3(e2[r] &= p.cc[g[r]][M][0])
+    GOL_ROWS3(c[r] = bitop3<TT_MUX>(t0[r], e1[r], e2[r]))
+#undef GOL_ROWS3
+}
+// All NSTG stages of one 3-row block (steps 0 .. NSTG + 1).
+template <int K, int NSTG, int... W>
+__device__ __forceinline__ void sstage_waves3(Pipe<K, 1> &p, uint32_t (&c)[3], std::integer_sequence<int, W...>)
+{
+    (sstage_wave3<K, NSTG, W>(p, c), ...);
 }
 
 // Work items of the pipelined kernels (one workgroup = one column group x one strip of rows).
@@ -892,6 +935,17 @@ __device__ __forceinline__ uint32_t pack32(const uint4 lo, const uint4 hi)
                                       false);
     return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
 }
+// Same for bytes that are exactly 0x00 or 0xFF (-1 as int8): weights -2^i give +2^i per set byte.
+__device__ __forceinline__ uint32_t pack32_ff(const uint4 lo, const uint4 hi)
+{
+    const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        b[q] = (uint32_t)__builtin_amdgcn_sdot4((int)d[2 * q], (int)0xF8FCFEFFu,
+                                               __builtin_amdgcn_sdot4((int)d[2 * q + 1], (int)0x80C0E0F0u, 0, false), false);
+    return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+}
 
 __device__ __forceinline__ void unpack32(const uint32_t w, uint4 &lo, uint4 &hi)
 {
@@ -1022,15 +1076,23 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
         : "memory");
 }
 
-// 1-D grid of work items (work_item).
-template <int KW, int P>
+// 1-D grid of work items (work_item).  P waves of one column group: wave 0 loads its input
+// byte rows (one 3-row block ahead, in registers) and packs them with v_dot4_i32_i8, runs KF
+// stages and hands the block on; waves 1 .. P-2 run KM stages each; wave P-1 runs KL stages,
+// realigns the frame, unpacks through a 2 KiB LDS table (byte value -> 8 bytes of 0x00 / 0xFF)
+// and stores.  The first and last waves carry the byte conversion, so they get fewer stages
+// (a wave that is busy when its consumer wants the next block sets the pipeline's rate).
+// One loop per role (no role branches inside the loop).
+template <int KF, int KM, int KL, int P>
 __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 {
-    constexpr int K = KW * P;
+    constexpr int K = KF + (P - 2) * KM + KL;
+    constexpr int KX = KM > KF ? (KM > KL ? KM : KL) : (KF > KL ? KF : KL);
     static_assert(K <= 32, "one 32-cell halo word per side");
     constexpr int NS = 3;
     constexpr int ROW = 64;  // uint32 per LDS row
     __shared__ uint32_t ring[P - 1][NS][3][ROW];
+    __shared__ uint2 lut[256];
     __shared__ int ready[P], consumed[P];
 
     const int lane = threadIdx.x & 63;
@@ -1060,15 +1122,15 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
         r.lo = q[0];
         r.hi = q[1];
     };
-    auto store = [&](char *row, uint32_t nbytes, const uint32_t w) {  // wave P-1
-        uint4 lo, hi;
-        unpack32(w, lo, hi);
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, (int)nbytes, 0x00020000);
-        typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{lo.x, lo.y, lo.z, lo.w}, r, st_off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, hi.z, hi.w}, r, st_off + 16u, 0, 0);
-    };
-
+    for (int i = threadIdx.x; i < 256; i += 64 * P) {
+        uint32_t o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t sp = __umul24((i >> (4 * h)) & 0xF, 0x00204081u) & 0x01010101u;
+            o[h] = (sp << 8) - sp;
+        }
+        lut[i] = make_uint2(o[0], o[1]);
+    }
     if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
     __syncthreads();
     lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
@@ -1078,85 +1140,70 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
         return ring_l + (((e - 1) * NS + b % NS) * 3 + S) * ROW + lane;
     };
 
-    Pipe<KW, 1> p;
+    Pipe<KX, 1> p;
     pipe_init(p);
-    // wave 0: the raw bytes of one block in registers (8 VGPRs per row), packed to 3 words
-    // before the next block's loads are issued into the same registers
-    Raw32 buf[3];
-    if (wv == 0) {
-#pragma unroll
-        for (int s = 0; s < 3; ++s) load(first_in + s, buf[s]);
-    }
     uint32_t alive = 0;
-    bool ok = true;
-    int seen_ready = 0, seen_free = 0;
     const uint32_t nrows = (uint32_t)(s1 - s0);
-    char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch;
-    auto block = [&](int b) {
-        uint32_t rows3[3] = {0, 0, 0};
-        if (wv == 0) {
+    auto run = [&](auto role_c) -> bool {
+        constexpr int ROLE = decltype(role_c)::value;  // 0 first, 1 middle, 2 last
+        constexpr int NSTG = ROLE == 0 ? KF : (ROLE == 2 ? KL : KM);
+        int seen_ready = 0, seen_free = 0;
+        char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch;
+        Raw32 buf[3];
+        if constexpr (ROLE == 0) {
 #pragma unroll
-            for (int s = 0; s < 3; ++s) rows3[s] = pack32(buf[s].lo, buf[s].hi);
-#pragma unroll
-            for (int s = 0; s < 3; ++s) load(first_in + 3 * (b + 1) + s, buf[s]);  // clamped past the end
-        } else if (seen_ready < b + 1) {
-            seen_ready = spin_until_ge(ready_l + wv, b + 1);
-            ok = seen_ready >= 0;
-            if (!ok) return;
+            for (int S = 0; S < 3; ++S) load(first_in + S, buf[S]);
         }
-        // the block's three rows, read and waited for in one asm statement: a split issue /
-        // wait lets the compiler copy the destination VGPR while the read is in flight (it did
-        // here; tools/check_lds_wait.py scans the assembly for that)
-        if (wv != 0) {
-            lds_rd32x3(slot_row(wv, b, 0), rows3);
-            if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
-        }
-        // the three rows' stages first, one basic block the scheduler can interleave (stage g
-        // of row S+1 is independent of stage g+1 of row S), then the stores / ring writes
-        uint32_t outw[3];
+        for (int b = 0; b < nblk; ++b) {
+            uint32_t w3[3];
+            if constexpr (ROLE == 0) {
 #pragma unroll
-        for (int S = 0; S < 3; ++S) {
-            uint32_t cur[1] = {rows3[S]};
+                for (int S = 0; S < 3; ++S) w3[S] = pack32_ff(buf[S].lo, buf[S].hi);
 #pragma unroll
-            for (int g = 0; g < KW; ++g) {
-                if (S == 0) sstage<KW, 1, 0>(p, g, cur);
-                if (S == 1) sstage<KW, 1, 1>(p, g, cur);
-                if (S == 2) sstage<KW, 1, 2>(p, g, cur);
+                for (int S = 0; S < 3; ++S) load(first_in + 3 * (b + 1) + S, buf[S]);  // clamped past the end
+            } else {
+                if (seen_ready < b + 1) {
+                    seen_ready = spin_until_ge(ready_l + wv, b + 1);
+                    if (seen_ready < 0) return false;
+                }
+                // read and waited for in one asm statement (see lds_rd32x3)
+                lds_rd32x3(slot_row(wv, b, 0), w3);
+                if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
             }
-            outw[S] = cur[0];
-        }
-        if (wv == P - 1) {
+            sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
+            if constexpr (ROLE == 2) {
 #pragma unroll
-            for (int S = 0; S < 3; ++S) {
-                const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
-                // takes its shift mod 32)
-                const uint32_t nx = from_upper_lane(outw[S]);
-                const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, outw[S], K % 32) : nx;
-                store(srow, row_ok ? row_bytes : 0u, o);
-                srow += pitch;
-                if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
-            }
-        } else {
-            if (seen_free < b + 1 - NS) {
-                seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
-                ok = seen_free >= 0;
-                if (!ok) return;
-            }
+                for (int S = 0; S < 3; ++S) {
+                    // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
+                    // takes its shift mod 32)
+                    const uint32_t nx = from_upper_lane(w3[S]);
+                    const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, w3[S], K % 32) : nx;
+                    const uint2 e0 = lut[o & 0xFF], e1 = lut[(o >> 8) & 0xFF], e2 = lut[(o >> 16) & 0xFF], e3 = lut[o >> 24];
+                    const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
+                    const __amdgpu_buffer_rsrc_t r =
+                        __builtin_amdgcn_make_buffer_rsrc(srow, (short)0, (int)(row_ok ? row_bytes : 0u), 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e0.x, e0.y, e1.x, e1.y}, r, st_off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e2.x, e2.y, e3.x, e3.y}, r, st_off + 16u, 0, 0);
+                    srow += pitch;
+                    if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
+                }
+            } else {
+                if (seen_free < b + 1 - NS) {
+                    seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    if (seen_free < 0) return false;
+                }
 #pragma unroll
-            for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)outw[S]);
+                for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)w3[S]);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
+            }
         }
-        if (wv < P - 1) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
-        }
+        return true;
     };
-    int b = 0;
-    for (; b + 1 < nblk && ok; b += 2) {  // two blocks per trip (the measured schedule)
-        block(b);
-        if (ok) block(b + 1);
-    }
-    if (b < nblk && ok) block(b);
+    bool ok;
+    if (wv == 0) ok = run(std::integral_constant<int, 0>());
+    else if (wv == P - 1) ok = run(std::integral_constant<int, 2>());
+    else ok = run(std::integral_constant<int, 1>());
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
     if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }
@@ -1690,6 +1737,16 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
 static const double BAND_PIPE_RANK_W[4] = {GOL_BAND_RANK_W};
 static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 
+// k = 32 on byte boards: stages of the first / middle / last waves and the wave count.  Equal
+// stages measured best: 16384^2, same box, 4/4/4 x 8 waves 47.7 TCUPS; 3/4/5 x 8 43.5; 1/5/1 x 8
+// 43.5; 2/4/2 x 9 43.6; 1/4/3 x 9 42.8; 3/5/4 x 7 42.0; 2/5/5 x 7 41.3; 4/6/4 x 6 41.8.
+#ifndef GOL_BYTES_PIPE_STAGES
+#define GOL_BYTES_PIPE_STAGES 4, 4, 4
+#define GOL_BYTES_PIPE_P 8
+#endif
+#define BYTES_PIPE (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P>)
+static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
+
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
@@ -1798,14 +1855,14 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
     if (!a.err) return hipErrorOutOfMemory;
     a.sm = StripMap{};
     if (k == 32) {
-        // one workgroup of 8 waves x 4 turns per (column group, strip): rank-weighted strips in
-        // one round, else round-tiled strips >= 4k rows
-        const void *kf = (const void *)bytes_pipe_kernel<4, 8>;
+        // one workgroup of GOL_BYTES_PIPE_P waves per (column group, strip): rank-weighted strips
+        // in one round, else round-tiled strips >= 4k rows
+        const void *kf = (const void *)BYTES_PIPE;
         const int cus = device_cus();
-        const int64_t slots = resident_workgroups(kf, 512);
+        const int64_t slots = resident_workgroups(kf, 64 * BYTES_PIPE_P);
         int64_t nwg = 0;
         if (strip <= 0 && cus > 0 &&
-            rank_split(rows, a.ngroups, cus, (int)(slots / cus), BYTES_PIPE_RANK_W, 4 * k, 1024, a.sm)) {
+            rank_split(rows, a.ngroups, cus, (int)(slots / cus), BYTES_PIPE_RANK_W, 2 * k, 1024, a.sm)) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
             if (strip <= 0) {
@@ -1814,7 +1871,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
             }
             nwg = (int64_t)a.ngroups * ((rows + a.strip - 1) / a.strip);
         }
-        hipLaunchKernelGGL((bytes_pipe_kernel<4, 8>), dim3((unsigned)nwg), dim3(512), 0, s, a);
+        hipLaunchKernelGGL(BYTES_PIPE, dim3((unsigned)nwg), dim3(64 * BYTES_PIPE_P), 0, s, a);
         return hipGetLastError();
     }
     const int nstrips = (int)((rows + a.strip - 1) / a.strip);

@@ -18,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "tl")
-LIB = os.path.join(ROOT, "tools", "tl", "libtimeline.so")
+LIB = os.environ.get("GOL_TL_LIB") or os.path.join(ROOT, "tools", "tl", "libtimeline.so")
 
 ENTRY = "    const int lane = threadIdx.x & 63;\n"
 STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n"
@@ -31,7 +31,11 @@ STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear w
         const uint64_t i = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if ((threadIdx.x & 63) == 0) {
             a.slots[4 * i] = tl_t0; a.slots[4 * i + 1] = tl_t1;
+#ifdef GOL_EXP_PROF
+            a.slots[4 * i + 2] = prof_a; a.slots[4 * i + 3] = prof_b; (void)hw; (void)xcc;
+#else
             a.slots[4 * i + 2] = hw; a.slots[4 * i + 3] = xcc;
+#endif
         }
         (void)alive;
     }

@@ -16,11 +16,11 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
     __shared__ uint32_t ring[4][3][3][256];
     lds_u32 *const slot = (lds_u32 *)&ring[threadIdx.x >> 6][0][0][0] + (threadIdx.x & 63) * 4;
     v4u32 nextv = v4u32{threadIdx.x, 1u, 2u, 3u};
-    if (MODE & 1) lds_wr128(slot, nextv);
-    if (MODE & 1) nextv = lds_rd128_issue(slot);
+    if (MODE & 1) lds_wr128_o<0>(slot, nextv);
+    if (MODE & 1) nextv = lds_rd128_issue_o<0>(slot);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);  // range 0: dropped
     Pipe<KW, DW> p;
-    PipeSel<KW, DW, 0>::init(p);
+    pipe_init(p);
     uint32_t seed = threadIdx.x * 2654435761u + blockIdx.x;
     uint32_t acc = 0;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -31,7 +31,7 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
             if (MODE & 1) {
                 lds_wait_n<1>(nextv);
                 const v4u32 v = nextv;
-                nextv = lds_rd128_issue(slot + ((S + 1) % 3) * 256);
+                nextv = lds_rd128_issue_o<0>(slot + ((S + 1) % 3) * 256);
 #pragma unroll
                 for (int j = 0; j < DW; ++j) cur[j] = v[j] ^ (it * 3 + S + j);
             } else {
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
             }
 #pragma unroll
             for (int j = 0; j < DW; ++j) acc ^= cur[j];
-            if (MODE & 1) lds_wr128(slot + S * 256, v4u32{cur[0], cur[1], cur[2], cur[3]});
+            if (MODE & 1) lds_wr128_o<0>(slot + S * 256, v4u32{cur[0], cur[1], cur[2], cur[3]});
             if (MODE & 2) {
                 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
                 __builtin_amdgcn_raw_buffer_store_b128(v4u{cur[0], cur[1], cur[2], cur[3]}, rs, (threadIdx.x & 63) * 16, 0, 0);
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
         }
     }
     if (MODE & 1) {
-        lds_wait(nextv);
+        lds_wait_n<0>(nextv);
         acc ^= nextv.x;
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
