@@ -235,9 +235,18 @@ __device__ __forceinline__ void sstage_waves3(Pipe<K, 1> &p, uint32_t (&c)[3], s
 // so the CU's workgroups run at different speeds (one round of equal strips ended them at 247 /
 // 298 / 388 / 482 us, tools/timeline.py); each CU then takes one column group x `period` rows
 // and splits the rows by arrival rank: rank r gets len[r] rows at off[r].
+// Paired ranks (dir != 0): two workgroups of a CU share one row range [off, off + len) and
+// walk it from both ends (dir +1 down from its top, dir -1 up from its bottom), claiming input
+// blocks from a counter of the pair (claims: 16 words per (CU, pair slot): [0] blocks claimed,
+// [1] pipelines done; the second to finish zeroes both for the next launch).  3 * (claimed
+// blocks of both) = len + 4K exactly, so their outputs meet without overlap wherever the
+// faster one got to: no rank waits for a slower one at the end of the launch.
 struct StripMap {
     int32_t ranked, cus, per_cu, period;
     int32_t len[4], off[4];
+    int32_t dir[4], pslot[4];
+    uint32_t *claims;
+    int32_t chunk;  // blocks per claim
 };
 
 struct BitsArgs {
@@ -277,6 +286,16 @@ __device__ __forceinline__ bool work_item(const StripMap &sm, int ngroups, int64
         rot = rank;
     }
     return s0 < s1;
+}
+// Direction and claim counter of workgroup l (0 / nullptr: a static strip).
+__device__ __forceinline__ int work_dir(const StripMap &sm, int l, uint32_t *&ctr)
+{
+    ctr = nullptr;
+    if (!sm.ranked) return 0;
+    const int rank = l / sm.cus, c = l % sm.cus;
+    if (!sm.dir[rank]) return 0;
+    ctr = sm.claims + ((int64_t)c * 2 + sm.pslot[rank]) * 16;
+    return sm.dir[rank];
 }
 
 // ------------------------------------------------------------------ bit-board step, standard layout
@@ -1099,12 +1118,17 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int group, s0, s1, rotv;
     if (!work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv)) return;
+    uint32_t *ctr;
+    const int dir = work_dir(a.sm, blockIdx.x, ctr);  // 0: static strip, +1 / -1: paired
     const int64_t col_raw = (int64_t)group * 62 + (lane - 1);
     const int64_t col = ((col_raw % a.Wd) + a.Wd) % a.Wd;
     const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
     const int R = (int)a.R;
     const int first_in = s0 - K, last_in = s1 + K - 1;
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
+    // a pair's range, stretched to s1e so that 3 blocks divide its len + 4K (rows past s1 are
+    // read clamped and never stored: they only feed outputs past s1)
+    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + 2) / 3) * 3 - 4 * K : s1;
     const int pitch = (int)a.pitch;
     const char *mid_b = reinterpret_cast<const char *>(a.mid);
     const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch;
@@ -1115,8 +1139,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
 
-    auto load = [&](int y, Raw32 &r) {  // wave 0
-        y = y > last_in ? last_in : y;
+    // stream position t (input row index of this pipeline) -> input row / output row
+    auto in_row = [&](int t) { return dir >= 0 ? first_in + t : s1e + K - 1 - t; };
+    auto out_row = [&](int t) { return dir >= 0 ? s0 + t - 2 * K : s1e - 1 + 2 * K - t; };
+    auto load = [&](int t, Raw32 &r) {  // wave 0
+        int y = in_row(t);
+        y = y > last_in ? last_in : (y < first_in ? first_in : y);  // past the end: clamped, never stored
         const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
         const uint4 *q = reinterpret_cast<const uint4 *>(mid_b + (d + (int64_t)y * pitch) + lane_off);
         r.lo = q[0];
@@ -1144,28 +1172,54 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     pipe_init(p);
     uint32_t alive = 0;
     const uint32_t nrows = (uint32_t)(s1 - s0);
+    // ready flags count published blocks; the first wave ends the stream with FINAL | blocks,
+    // which every wave passes on after its last block (a paired pipeline learns its block count
+    // only when a claim fails)
+    constexpr int FINAL = 1 << 30;
+    const int nclaim = (s1e - s0 + 4 * K) / 3;  // blocks of the pair
+    const int chunk = a.sm.chunk;
     auto run = [&](auto role_c) -> bool {
         constexpr int ROLE = decltype(role_c)::value;  // 0 first, 1 middle, 2 last
         constexpr int NSTG = ROLE == 0 ? KF : (ROLE == 2 ? KL : KM);
         int seen_ready = 0, seen_free = 0;
-        char *srow = dst_b + (int64_t)(s0 - 2 * K) * pitch;
         Raw32 buf[3];
+        int nb = nblk;        // role 0: blocks granted so far
+        uint32_t next = 0;    // role 0, paired: blocks claimed before the pending claim
         if constexpr (ROLE == 0) {
+            if (dir) {
+                uint32_t c0 = 0;
+                if (lane == 0) c0 = atomicAdd(ctr, (uint32_t)chunk);
+                c0 = __builtin_amdgcn_readfirstlane(c0);
+                nb = c0 >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c0);
+                if (nb == chunk) {
+                    if (lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);  // prefetched claim
+                }
+            }
 #pragma unroll
-            for (int S = 0; S < 3; ++S) load(first_in + S, buf[S]);
+            for (int S = 0; S < 3; ++S) load(S, buf[S]);
         }
-        for (int b = 0; b < nblk; ++b) {
+        int b = 0;
+        for (;; ++b) {
             uint32_t w3[3];
             if constexpr (ROLE == 0) {
+                if (b >= nb) {
+                    if (!dir || nb % chunk != 0 || nb == 0) break;
+                    const uint32_t c = __builtin_amdgcn_readfirstlane(next);
+                    const int g = c >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c);
+                    if (g == 0) break;
+                    nb += g;
+                    if (g == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);
+                }
 #pragma unroll
                 for (int S = 0; S < 3; ++S) w3[S] = pack32_ff(buf[S].lo, buf[S].hi);
 #pragma unroll
-                for (int S = 0; S < 3; ++S) load(first_in + 3 * (b + 1) + S, buf[S]);  // clamped past the end
+                for (int S = 0; S < 3; ++S) load(3 * (b + 1) + S, buf[S]);  // clamped past the end
             } else {
                 if (seen_ready < b + 1) {
                     seen_ready = spin_until_ge(ready_l + wv, b + 1);
                     if (seen_ready < 0) return false;
                 }
+                if (seen_ready >= FINAL && b >= seen_ready - FINAL) break;
                 // read and waited for in one asm statement (see lds_rd32x3)
                 lds_rd32x3(slot_row(wv, b, 0), w3);
                 if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
@@ -1179,12 +1233,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                     const uint32_t nx = from_upper_lane(w3[S]);
                     const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, w3[S], K % 32) : nx;
                     const uint2 e0 = lut[o & 0xFF], e1 = lut[(o >> 8) & 0xFF], e2 = lut[(o >> 16) & 0xFF], e3 = lut[o >> 24];
-                    const bool row_ok = (uint32_t)(3 * b + S - 2 * K) < nrows;
-                    const __amdgpu_buffer_rsrc_t r =
-                        __builtin_amdgcn_make_buffer_rsrc(srow, (short)0, (int)(row_ok ? row_bytes : 0u), 0x00020000);
+                    const int y = out_row(3 * b + S);
+                    const bool row_ok = (uint32_t)(y - s0) < nrows;
+                    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                        dst_b + (int64_t)(row_ok ? y : s0) * pitch, (short)0, (int)(row_ok ? row_bytes : 0u), 0x00020000);
                     __builtin_amdgcn_raw_buffer_store_b128(v4u32{e0.x, e0.y, e1.x, e1.y}, r, st_off, 0, 0);
                     __builtin_amdgcn_raw_buffer_store_b128(v4u32{e2.x, e2.y, e3.x, e3.y}, r, st_off + 16u, 0, 0);
-                    srow += pitch;
                     if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
                 }
             } else {
@@ -1196,6 +1250,19 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                 for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)w3[S]);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
+            }
+        }
+        if constexpr (ROLE != 2) {
+            if (lane == 0) lds_wr32(ready_l + wv + 1, FINAL + b);
+        }
+        if constexpr (ROLE == 0) {
+            if (dir && lane == 0) {
+                // this pipeline's claims are over (none in flight): the second of the pair to get
+                // here zeroes the counters for the next launch
+                if (atomicAdd(ctr + 1, 1u) == 1u) {
+                    atomicExch(ctr, 0u);
+                    atomicExch(ctr + 1, 0u);
+                }
             }
         }
         return true;
@@ -1693,8 +1760,31 @@ static int device_cus()
 // the measured relative speed of the rank-th arrival on a CU.  Used when the strips of one
 // column group can be spread over the CUs with little waste (ngroups x strips per group >= 94 %
 // of the CUs) and every rank still gets >= min_rows rows; else false (equal strips).
+// Claim counters of the paired ranks (StripMap), one zeroed buffer per stream: launches on one
+// stream run in order and leave their counters zeroed; launches on different streams may run
+// at once and must not share counters.
+static uint32_t *claim_counters(hipStream_t s, int cus)
+{
+    static std::mutex mu;
+    static std::map<std::pair<hipStream_t, int>, uint32_t *> bufs;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = bufs.find({s, dev});
+    if (it != bufs.end()) return it->second;
+    uint32_t *c = nullptr;
+    const size_t bytes = (size_t)cus * 2 * 16 * sizeof(uint32_t);
+    if (hipMalloc(&c, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(c, 0, bytes) != hipSuccess) {
+        (void)hipFree(c);
+        return nullptr;
+    }
+    bufs[{s, dev}] = c;
+    return c;
+}
+
 static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const double *weight, int64_t min_rows,
-                       int64_t max_strip, StripMap &sm)
+                       int64_t max_strip, StripMap &sm, uint32_t *claims = nullptr, int chunk = 0)
 {
     if (cus <= 0 || cus % 8 || per_cu < 1 || per_cu > 4 || ngroups > cus || rows <= 0) return false;
     // only boards that fill the device at most twice with strips of max_strip rows: on bigger
@@ -1710,6 +1800,40 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
     m.cus = cus;
     m.per_cu = per_cu;
     m.period = (int32_t)period;
+    if (claims && per_cu >= 2) {
+        // pairs walking one range from both ends: per_cu 2: (0, 1); 3: (0, 2) + rank 1 alone;
+        // 4: (0, 3) + (1, 2).  A pair's range gets the sum of its ranks' weights.
+        static const int pa[4][2] = {{0, 0}, {0, 0}, {0, 1}, {0, 2}};
+        int ga[2][2];
+        int ng = 0;
+        if (per_cu == 4) { ga[0][0] = 0; ga[0][1] = 3; ga[1][0] = 1; ga[1][1] = 2; ng = 2; }
+        else { ga[0][0] = pa[per_cu][0]; ga[0][1] = pa[per_cu][1]; ng = 1; }
+        m.claims = claims;
+        m.chunk = chunk;
+        int64_t off = 0;
+        double wused = 0;
+        for (int g = 0; g < ng; ++g) {
+            const double w = weight[ga[g][0]] + weight[ga[g][1]];
+            wused += w;
+            const int64_t len = (g == ng - 1 && per_cu != 3) ? period - off : (int64_t)(period * wused / wsum + 0.5) - off;
+            if (len < min_rows) return false;
+            for (int j = 0; j < 2; ++j) {
+                const int r = ga[g][j];
+                m.off[r] = (int32_t)off;
+                m.len[r] = (int32_t)len;
+                m.dir[r] = j == 0 ? 1 : -1;
+                m.pslot[r] = g;
+            }
+            off += len;
+        }
+        if (per_cu == 3) {  // rank 1: the rest, a static strip
+            if (period - off < min_rows) return false;
+            m.off[1] = (int32_t)off;
+            m.len[1] = (int32_t)(period - off);
+        }
+        sm = m;
+        return true;
+    }
     int64_t off = 0;
     for (int r = 0; r < per_cu; ++r) {
         const int64_t len = r == per_cu - 1 ? period - off : (int64_t)(period * weight[r] / wsum + 0.5);
@@ -1740,6 +1864,9 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 // k = 32 on byte boards: stages of the first / middle / last waves and the wave count.  Equal
 // stages measured best: 16384^2, same box, 4/4/4 x 8 waves 47.7 TCUPS; 3/4/5 x 8 43.5; 1/5/1 x 8
 // 43.5; 2/4/2 x 9 43.6; 1/4/3 x 9 42.8; 3/5/4 x 7 42.0; 2/5/5 x 7 41.3; 4/6/4 x 6 41.8.
+#ifndef GOL_BYTES_PAIRED
+#define GOL_BYTES_PAIRED 1
+#endif
 #ifndef GOL_BYTES_PIPE_STAGES
 #define GOL_BYTES_PIPE_STAGES 4, 4, 4
 #define GOL_BYTES_PIPE_P 8
@@ -1861,8 +1988,9 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         const int cus = device_cus();
         const int64_t slots = resident_workgroups(kf, 64 * BYTES_PIPE_P);
         int64_t nwg = 0;
+        uint32_t *claims = GOL_BYTES_PAIRED ? claim_counters(s, cus) : nullptr;
         if (strip <= 0 && cus > 0 &&
-            rank_split(rows, a.ngroups, cus, (int)(slots / cus), BYTES_PIPE_RANK_W, 2 * k, 1024, a.sm)) {
+            rank_split(rows, a.ngroups, cus, (int)(slots / cus), BYTES_PIPE_RANK_W, 2 * k, 1024, a.sm, claims, 4)) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
             if (strip <= 0) {
