@@ -685,6 +685,8 @@ band_pipe_kernel(BitsArgs a)
     const int lane = threadIdx.x & 63;
     int group, s0, s1, rotv;
     const bool has_rows = work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv);
+    uint32_t *ctr;
+    const int dir = work_dir(a.sm, blockIdx.x, ctr);  // 0: static strip, +1 / -1: paired (StripMap)
     // Pipeline position of this wave, rotated per workgroup: the waves of a workgroup sit on the
     // CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put its
     // loader (global_load_lds) on one SIMD and its storer on another.
@@ -701,6 +703,10 @@ band_pipe_kernel(BitsArgs a)
     const int first_in = s0 - K;
     const int last_in = s1 + K - 1;
     const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
+    // a pair's range, stretched to s1e so that 9 (3 blocks of 3 rows: one loop trip) divide its
+    // len + 4K; rows past s1 are read clamped and never stored
+    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + 8) / 9) * 9 - 4 * K : s1;
+    const int nclaim = (s1e - s0 + 4 * K) / 3;  // blocks of the pair (a multiple of 3)
 
     const int pitch_b = (int)a.pitch * 4;
     const char *mid_b = reinterpret_cast<const char *>(a.mid);
@@ -715,8 +721,9 @@ band_pipe_kernel(BitsArgs a)
     auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-            int y = first_in + 3 * b + s;
-            y = y > last_in ? last_in : y;
+            const int t = 3 * b + s;  // stream position
+            int y = dir >= 0 ? first_in + t : s1e + K - 1 - t;
+            y = y > last_in ? last_in : (y < first_in ? first_in : y);
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
@@ -781,18 +788,28 @@ band_pipe_kernel(BitsArgs a)
     // >= 2^32 - 2K * pitch) and from s1 on fall outside it, and so does a halo lane's 2^31.
     const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
         dst_b + (int64_t)s0 * pitch_b, (short)0, (int)(nrows * (uint32_t)pitch_b), 0x00020000);
-    uint32_t voff = st_off - (uint32_t)(2 * K) * (uint32_t)pitch_b;
-    int rrel = -2 * K;  // output row - s0 (wave-uniform)
+    // (walking up, dir -1: output row y = s1e - 1 + 2K - 3b - S, offsets decreasing)
+    int rrel = dir >= 0 ? -2 * K : s1e - 1 + 2 * K - s0;  // output row - s0 (wave-uniform)
+    const int rstep = dir >= 0 ? 1 : -1;
+    uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch_b;
+    const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch_b;
     auto emit = [&](const uint32_t (&cur)[DW]) {
         __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, 2);
         // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are masked
         // once at the end)
         if (a.slots && (uint32_t)rrel < nrows)
             alive += __popc(cur[0]) + __popc(cur[1]) + __popc(cur[2]) + __popc(cur[3]);
-        voff += (uint32_t)pitch_b;
-        ++rrel;
+        voff += vstep;
+        rrel += rstep;
     };
     lds_u32 *const src_base = wv == 0 ? in_base : rd_base;
+    // paired: the loader's claims, 3 blocks (one loop trip) each, one in flight (issued at row 2
+    // of a trip's first block, used at the next trip's start); the first before block 0's loads
+    constexpr int FINAL = 1 << 30;  // ready flag = FINAL + blocks: the stream has ended
+    // (lane 0 claims; the kernels are built without the atomic optimizer, which broadcast the
+    // claim's return at once and so waited for it right there: an atomic round trip per trip)
+    uint32_t pending = 0;
+    if (wv == 0 && dir && lane == 0) pending = atomicAdd(ctr, 3u);
     // block 0's row 0, read to completion here (the compiler copies the loop-carried register
     // on loop entry, which must not happen while a read is in flight)
     if (wv == 0) {
@@ -808,9 +825,12 @@ band_pipe_kernel(BitsArgs a)
     }
     v4u32 nextv = lds_rd128(src_base);
     lds_flag_wr(wv == 0 ? scratch : cns_addr, 0);  // one younger LDS operation for block 0's wait
-    auto step = [&](int b, auto u_c, auto role_c) -> bool {
+    // readers: the block the loop is about to run exists (an empty paired stream ends at once)
+    bool more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
+    auto step = [&](int b, auto u_c, auto role_c, auto dyn_c) -> bool {
         constexpr int US = decltype(u_c)::value;
         constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool DYN = decltype(dyn_c)::value;
         constexpr bool LAST = ROLE == 2;
         uint32_t cur[DW];
         auto realign = [&]() {
@@ -843,18 +863,23 @@ band_pipe_kernel(BitsArgs a)
         lds_wait_n<LAST ? 0 : 1>(nextv);
         unpack(nextv, cur);
         if constexpr (ROLE == 0) {
-            stage_in(b + 2, in_ring[(US + 2) % 3]);           // refills block b-1's slot (clamped past the end)
-            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // block b+1 landed, b+2 in flight
+            stage_in(b + 2, in_ring[(US + 2) % 3]);  // refills block b-1's slot (clamped past the end)
+            // block b+1 landed, b+2 in flight (and, paired, at US 1 the claim issued at US 0)
+            if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            if constexpr (DYN && US == 0) {
+                if (lane == 0) pending = atomicAdd(ctr, 3u);
+            }
             nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
             lds_flag_wr(scratch, 0);
         } else {
-            if (b + 1 < nblk3) {
-                if (seen_ready < b + 2) {
-                    seen_ready = spin_until_ge(ready_l + wv, b + 2);
-                    if (seen_ready < 0) return false;
-                }
-                nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
+            // the next block exists unless the writer's flag says the stream ended before it
+            if (seen_ready < b + 2) {
+                seen_ready = spin_until_ge(ready_l + wv, b + 2);
+                if (seen_ready < 0) return false;
             }
+            more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
+            if (more) nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
             lds_flag_wr(cns_addr, b + 1);
         }
         realign();
@@ -863,22 +888,43 @@ band_pipe_kernel(BitsArgs a)
         else lds_wr128_o<US * SB + 2 * RB>(wr_base, pack(cur));
         return true;
     };
-    auto run = [&](auto role_c) -> bool {
-        for (int b = 0; b < nblk3; b += 3) {
-            if (!step(b, std::integral_constant<int, 0>(), role_c)) return false;
-            if (!step(b + 1, std::integral_constant<int, 1>(), role_c)) return false;
-            if (!step(b + 2, std::integral_constant<int, 2>(), role_c)) return false;
+    // blocks the loader has: nblk3, or (paired) the claims granted so far
+    auto grant = [&](uint32_t c) { return c >= (uint32_t)nclaim ? 0 : 3; };
+    auto run = [&](auto role_c, auto dyn_c) -> bool {
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool DYN = decltype(dyn_c)::value;
+        int nb = DYN ? 0 : nblk3;
+        int b = 0;
+        for (;; b += 3) {
+            if constexpr (ROLE == 0) {
+                if constexpr (DYN) nb += grant(__builtin_amdgcn_readfirstlane(pending));
+                if (b >= nb) break;
+            } else {
+                if (!more) break;
+            }
+            if (!step(b, std::integral_constant<int, 0>(), role_c, dyn_c)) return false;
+            if (!step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c)) return false;
+            if (!step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c)) return false;
         }
-        if constexpr (decltype(role_c)::value != 2) {
+        if constexpr (ROLE != 2) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_flag_wr(rdy_addr, nblk3);
+            lds_flag_wr(rdy_addr, FINAL + b);
+        }
+        if constexpr (ROLE == 0 && DYN) {
+            if (lane == 0 && atomicAdd(ctr + 1, 1u) == 1u) {  // both loaders' claims are over
+                atomicExch(ctr, 0u);
+                atomicExch(ctr + 1, 0u);
+            }
         }
         return true;
     };
+    auto run_role = [&](auto role_c) -> bool {
+        return dir ? run(role_c, std::true_type()) : run(role_c, std::false_type());
+    };
     bool ok;
-    if (wv == 0) ok = run(std::integral_constant<int, 0>());
-    else if (wv == P - 1) ok = run(std::integral_constant<int, 2>());
-    else ok = run(std::integral_constant<int, 1>());
+    if (wv == 0) ok = run_role(std::integral_constant<int, 0>());
+    else if (wv == P - 1) ok = run_role(std::integral_constant<int, 2>());
+    else ok = run_role(std::integral_constant<int, 1>());
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
     alive &= st_mask;  // halo lanes' rows are not this group's
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1187,13 +1233,13 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
         uint32_t next = 0;    // role 0, paired: blocks claimed before the pending claim
         if constexpr (ROLE == 0) {
             if (dir) {
+                // lane 0 claims (see band_pipe_kernel); a claim's return is waited for where it
+                // is used
                 uint32_t c0 = 0;
                 if (lane == 0) c0 = atomicAdd(ctr, (uint32_t)chunk);
                 c0 = __builtin_amdgcn_readfirstlane(c0);
                 nb = c0 >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c0);
-                if (nb == chunk) {
-                    if (lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);  // prefetched claim
-                }
+                if (nb == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);  // prefetched claim
             }
 #pragma unroll
             for (int S = 0; S < 3; ++S) load(S, buf[S]);
@@ -1864,6 +1910,9 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 // k = 32 on byte boards: stages of the first / middle / last waves and the wave count.  Equal
 // stages measured best: 16384^2, same box, 4/4/4 x 8 waves 47.7 TCUPS; 3/4/5 x 8 43.5; 1/5/1 x 8
 // 43.5; 2/4/2 x 9 43.6; 1/4/3 x 9 42.8; 3/5/4 x 7 42.0; 2/5/5 x 7 41.3; 4/6/4 x 6 41.8.
+#ifndef GOL_BAND_PAIRED
+#define GOL_BAND_PAIRED 1
+#endif
 #ifndef GOL_BYTES_PAIRED
 #define GOL_BYTES_PAIRED 1
 #endif
@@ -1883,7 +1932,8 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
     const int cus = device_cus();
     const int64_t slots = resident_workgroups(kf, 64 * P);
     if (auto_strip && cus > 0 &&
-        rank_split(a.rows, a.ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, a.sm)) {
+        rank_split(a.rows, a.ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, a.sm,
+                   GOL_BAND_PAIRED ? claim_counters(s, cus) : nullptr, 3)) {
         nwg = (int64_t)cus * a.sm.per_cu;
     } else {
         if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);

@@ -26,6 +26,7 @@ CSRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
 
 def compile_asm(out):
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",  # as the Makefile's KFLAGS
                     "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "--cuda-device-only", "-S",
                     os.path.join(CSRC, "gol_kernels.hip"), "-o", out], check=True,
                    stderr=subprocess.DEVNULL)
