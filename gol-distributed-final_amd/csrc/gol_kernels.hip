@@ -241,12 +241,16 @@ __device__ __forceinline__ void sstage_waves3(Pipe<K, 1> &p, uint32_t (&c)[3], s
 // [1] pipelines done; the second to finish zeroes both for the next launch).  3 * (claimed
 // blocks of both) = len + 4K exactly, so their outputs meet without overlap wherever the
 // faster one got to: no rank waits for a slower one at the end of the launch.
+// Tail (ranked = 0, launches of many rounds): workgroups l >= tail_l, the last dispatched,
+// take strips of tail_strip rows from row tail_row on, so the launch ends on short strips
+// instead of a partial round of full ones.
 struct StripMap {
     int32_t ranked, cus, per_cu, period;
     int32_t len[4], off[4];
     int32_t dir[4], pslot[4];
     uint32_t *claims;
     int32_t chunk;  // blocks per claim
+    int32_t tail_l, tail_row, tail_strip;
 };
 
 struct BitsArgs {
@@ -265,16 +269,23 @@ __device__ __forceinline__ bool work_item(const StripMap &sm, int ngroups, int64
                                           int &group, int &s0, int &s1, int &rot)
 {
     const int end = (int)(row0 + rows);
-    if (!sm.ranked) {
+    if (!sm.ranked && sm.tail_l && l >= sm.tail_l) {
+        const int i = l - sm.tail_l;
+        group = i % ngroups;
+        const int t = i / ngroups;
+        s0 = (int)row0 + sm.tail_row + t * sm.tail_strip;
+        s1 = min(s0 + sm.tail_strip, end);
+        rot = group + t;
+    } else if (!sm.ranked) {
         // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (L2 per XCD), so
         // consecutive ids are remapped to let each XCD walk its own contiguous run of column groups
         // of a strip: the lateral halo columns two neighbouring groups both read then meet in one L2.
-        const int n = gridDim.x, per = n / 8;
+        const int n = sm.tail_l ? sm.tail_l : (int)gridDim.x, per = n / 8;
         const int m = l < per * 8 ? (l % 8) * per + l / 8 : l;
         group = m % ngroups;
         const int by = m / ngroups;
         s0 = (int)row0 + by * strip;
-        s1 = min(s0 + strip, end);
+        s1 = min(s0 + strip, sm.tail_l ? (int)row0 + sm.tail_row : end);
         rot = group + by;
     } else {
         const int rank = l / sm.cus, c = l % sm.cus;
@@ -1894,12 +1905,13 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
 
 // Rows per arrival rank, from measurements (tools/timeline.py, same-box A/B with tools/ab.py):
 // one round of equal strips ended the ranks' workgroups at T_r (band 247 / 298 / 388 / 482 us,
-// bytes 96 / 136 / 174 us), so the first split gave rank r a share ~ 1 / T_r; re-measuring moved
-// rows from the late ranks to the early ones (w_r <- w_r T_mean / T_r).  65536^2 bits: 103.4 ->
-// 106.1 TCUPS; 16384^2 bytes: 43.9 -> 45.2.  (The ends of one rank still spread over ~40 us from
-// CU to CU, which a static split cannot absorb.)
+// bytes 96 / 136 / 174 us), so the static split gives rank r a share ~ 1 / T_r, refined by
+// re-measuring (w_r <- w_r T_mean / T_r).  With paired ranks (StripMap) only the sum over a
+// pair matters: band pairs (0, 3) and (1, 2) ran at equal speed (65536^2: 0.54 / 0.46 ended
+// them at 425 / 360 us; 50 / 50: 110.3 TCUPS vs 106.2 for the static split, same box); bytes
+// pair (0, 2) with rank 1 alone on 0.31 of the rows.
 #ifndef GOL_BAND_RANK_W
-#define GOL_BAND_RANK_W 0.42, 0.28, 0.18, 0.12
+#define GOL_BAND_RANK_W 0.25, 0.25, 0.25, 0.25
 #endif
 #ifndef GOL_BYTES_RANK_W
 #define GOL_BYTES_RANK_W 0.4457, 0.3094, 0.2449, 0.0
@@ -1907,9 +1919,11 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
 static const double BAND_PIPE_RANK_W[4] = {GOL_BAND_RANK_W};
 static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 
-// k = 32 on byte boards: stages of the first / middle / last waves and the wave count.  Equal
-// stages measured best: 16384^2, same box, 4/4/4 x 8 waves 47.7 TCUPS; 3/4/5 x 8 43.5; 1/5/1 x 8
-// 43.5; 2/4/2 x 9 43.6; 1/4/3 x 9 42.8; 3/5/4 x 7 42.0; 2/5/5 x 7 41.3; 4/6/4 x 6 41.8.
+// Rounds of half-length tail strips (StripMap.tail_*): same box, 2^17 x 2^20: none 137.2 TCUPS,
+// 0.5 round 138.8, 1.0 138.8, 1.5 138.6; 262144^2: 132.2 / 133.6 / 133.2 / 133.0.
+#ifndef GOL_BAND_TAIL
+#define GOL_BAND_TAIL 0.5
+#endif
 #ifndef GOL_BAND_PAIRED
 #define GOL_BAND_PAIRED 1
 #endif
@@ -1938,6 +1952,18 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
     } else {
         if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
         nwg = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
+        if (auto_strip && GOL_BAND_TAIL && slots > 0 && nwg > 4 * slots) {
+            // the last ~GOL_BAND_TAIL rounds of workgroups run strips of half the rows
+            const int64_t ts = std::max<int64_t>(8 * KW * P, a.strip / 2);
+            const int64_t nt = (int64_t)(GOL_BAND_TAIL * (double)slots / a.ngroups + 0.999);  // tail strips per group
+            const int64_t tail_rows = std::min<int64_t>(a.rows / 2, nt * ts);
+            const int64_t big = a.rows - tail_rows;
+            const int64_t nbig = (big + a.strip - 1) / a.strip;
+            a.sm.tail_l = (int32_t)(a.ngroups * nbig);
+            a.sm.tail_row = (int32_t)big;
+            a.sm.tail_strip = (int32_t)ts;
+            nwg = a.sm.tail_l + a.ngroups * ((tail_rows + ts - 1) / ts);
+        }
     }
     if (contig)
         hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);

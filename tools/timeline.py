@@ -42,9 +42,25 @@ STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear w
 }"""
 
 
+PROF_SPINS = (  # -DGOL_EXP_PROF: cycles each wave spends in its flag waits (ready -> a, free -> b)
+    ("seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);", "prof_b"),
+    ("seen_ready = spin_until_ge(ready_l + wv, b + 2);", "prof_a"),
+    ("seen_ready = spin_until_ge(ready_l + wv, b + 1);", "prof_a"),
+)
+
+
 def build(flags=""):
     os.makedirs(OUT, exist_ok=True)
     src = open(os.path.join(CSRC, "gol_kernels.hip")).read()
+    if "GOL_EXP_PROF" in flags:
+        for stmt, acc in PROF_SPINS:
+            assert stmt in src, stmt
+            src = src.replace(stmt, "{ const uint64_t pt_ = __builtin_amdgcn_s_memtime(); " + stmt +
+                              f" {acc} += __builtin_amdgcn_s_memtime() - pt_; }}")
+        for kern in ("band_pipe_kernel(BitsArgs a)", "bytes_pipe_kernel(BytesKArgs a)"):
+            i = src.index(kern)
+            j = src.index("    uint32_t alive = 0;\n", i)
+            src = src[:j] + "    uint64_t prof_a = 0, prof_b = 0;\n" + src[j:]
     for kern, exit_ in (("band_pipe_kernel(BitsArgs a)", EXIT_BAND), ("bytes_pipe_kernel(BytesKArgs a)", EXIT_BYTES)):
         i = src.index(kern)
         j = src.index(ENTRY, i)
