@@ -1952,7 +1952,7 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
     } else {
         if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
         nwg = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
-        if (auto_strip && GOL_BAND_TAIL && slots > 0 && nwg > 4 * slots) {
+        if (auto_strip && GOL_BAND_TAIL > 0 && slots > 0 && nwg > 4 * slots) {
             // the last ~GOL_BAND_TAIL rounds of workgroups run strips of half the rows
             const int64_t ts = std::max<int64_t>(8 * KW * P, a.strip / 2);
             const int64_t nt = (int64_t)(GOL_BAND_TAIL * (double)slots / a.ngroups + 0.999);  // tail strips per group
