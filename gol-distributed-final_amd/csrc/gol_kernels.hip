@@ -1152,6 +1152,34 @@ __device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
         : "memory");
 }
 
+// The same three reads without the wait, and the wait (the values are in-out operands, so no
+// use of them moves above it).
+__device__ __forceinline__ void lds_rd32x3_issue(const lds_u32 *p, uint32_t (&r)[3])
+{
+    asm volatile(
+        "ds_read_b32 %0, %3\n\t"
+        "ds_read_b32 %1, %3 offset:256\n\t"
+        "ds_read_b32 %2, %3 offset:512"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
+        : "v"(p)
+        : "memory");
+}
+__device__ __forceinline__ void lds_wait3(uint32_t (&r)[3])
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2])::"memory");
+}
+
+#ifndef GOL_BYTES_PER_CU
+#define GOL_BYTES_PER_CU 3  // workgroups per CU of a one-round launch
+#endif
+// Ring slots per inter-wave ring of the byte pipeline: 4 measured +1.5 % over 3 (16384^2, same
+// box); with the hand-off software-pipelined (reads one block ahead, no wait for own writes)
+// the byte pipeline ran within 2 % of the blocking version, and 4 x 8-stage waves equal to 8 x 4:
+// at ~0.45-0.49 of the VALU issue roof neither the hand-off nor the HBM streams (no loads and
+// no stores: +10 %) bound it.
+#ifndef GOL_BYTES_NS
+#define GOL_BYTES_NS 4
+#endif
 // 1-D grid of work items (work_item).  P waves of one column group: wave 0 loads its input
 // byte rows (one 3-row block ahead, in registers) and packs them with v_dot4_i32_i8, runs KF
 // stages and hands the block on; waves 1 .. P-2 run KM stages each; wave P-1 runs KL stages,
@@ -1165,11 +1193,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     constexpr int K = KF + (P - 2) * KM + KL;
     constexpr int KX = KM > KF ? (KM > KL ? KM : KL) : (KF > KL ? KF : KL);
     static_assert(K <= 32, "one 32-cell halo word per side");
-    constexpr int NS = 3;
+    constexpr int NS = GOL_BYTES_NS;
     constexpr int ROW = 64;  // uint32 per LDS row
     __shared__ uint32_t ring[P - 1][NS][3][ROW];
     __shared__ uint2 lut[256];
     __shared__ int ready[P], consumed[P];
+    __shared__ int flag_scratch[P][64];  // flag writes of lanes 1..63 (see lds_flag_wr)
 
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1224,6 +1253,9 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     auto slot_row = [&](int e, int b, int S) {  // ring e (input of wave e), e >= 1
         return ring_l + (((e - 1) * NS + b % NS) * 3 + S) * ROW + lane;
     };
+    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0][0] + wv * 64 + lane;
+    lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // ring wv+1 ready
+    lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // ring wv consumed
 
     Pipe<KX, 1> p;
     pipe_init(p);
@@ -1255,6 +1287,22 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 #pragma unroll
             for (int S = 0; S < 3; ++S) load(S, buf[S]);
         }
+        // Readers (waves 1 .. P-1): block b+1's rows are read at the end of block b (spinning
+        // there for its flag if needed) and waited for at the top of block b+1; a middle wave
+        // publishes "blocks < b ready" right after that wait, which also covers its writes of
+        // block b-1 (a wave's LDS operations complete in order), so no wave waits for its own
+        // writes.  The first wave publishes after its block's compute (its writes of the
+        // previous block are long done by then).
+        uint32_t nx[3] = {0, 0, 0};
+        bool more = true;
+        if constexpr (ROLE != 0) {
+            if (seen_ready < 1) {
+                seen_ready = spin_until_ge(ready_l + wv, 1);
+                if (seen_ready < 0) return false;
+            }
+            more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
+            if (more) lds_rd32x3_issue(slot_row(wv, 0, 0), nx);
+        }
         int b = 0;
         for (;; ++b) {
             uint32_t w3[3];
@@ -1272,14 +1320,11 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 #pragma unroll
                 for (int S = 0; S < 3; ++S) load(3 * (b + 1) + S, buf[S]);  // clamped past the end
             } else {
-                if (seen_ready < b + 1) {
-                    seen_ready = spin_until_ge(ready_l + wv, b + 1);
-                    if (seen_ready < 0) return false;
-                }
-                if (seen_ready >= FINAL && b >= seen_ready - FINAL) break;
-                // read and waited for in one asm statement (see lds_rd32x3)
-                lds_rd32x3(slot_row(wv, b, 0), w3);
-                if (lane == 0) lds_wr32(consumed_l + wv, b + 1);
+                if (!more) break;
+                lds_wait3(nx);  // block b's rows (and every older LDS operation of this wave)
+                w3[0] = nx[0]; w3[1] = nx[1]; w3[2] = nx[2];
+                lds_flag_wr(cns_addr, b + 1);
+                if constexpr (ROLE == 1) lds_flag_wr(rdy_addr, b);  // blocks < b: written and complete
             }
             sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
             if constexpr (ROLE == 2) {
@@ -1287,8 +1332,8 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                 for (int S = 0; S < 3; ++S) {
                     // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
                     // takes its shift mod 32)
-                    const uint32_t nx = from_upper_lane(w3[S]);
-                    const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nx, w3[S], K % 32) : nx;
+                    const uint32_t nxw = from_upper_lane(w3[S]);
+                    const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nxw, w3[S], K % 32) : nxw;
                     const uint2 e0 = lut[o & 0xFF], e1 = lut[(o >> 8) & 0xFF], e2 = lut[(o >> 16) & 0xFF], e3 = lut[o >> 24];
                     const int y = out_row(3 * b + S);
                     const bool row_ok = (uint32_t)(y - s0) < nrows;
@@ -1299,18 +1344,29 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                     if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
                 }
             } else {
+                if constexpr (ROLE == 0) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // block b-1's writes
+                    lds_flag_wr(rdy_addr, b);
+                }
                 if (seen_free < b + 1 - NS) {
                     seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
                     if (seen_free < 0) return false;
                 }
 #pragma unroll
                 for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)w3[S]);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) lds_wr32(ready_l + wv + 1, b + 1);
+            }
+            if constexpr (ROLE != 0) {
+                if (seen_ready < b + 2) {
+                    seen_ready = spin_until_ge(ready_l + wv, b + 2);
+                    if (seen_ready < 0) return false;
+                }
+                more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
+                if (more) lds_rd32x3_issue(slot_row(wv, b + 1, 0), nx);
             }
         }
         if constexpr (ROLE != 2) {
-            if (lane == 0) lds_wr32(ready_l + wv + 1, FINAL + b);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_flag_wr(rdy_addr, FINAL + b);
         }
         if constexpr (ROLE == 0) {
             if (dir && lane == 0) {
@@ -2066,7 +2122,8 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         int64_t nwg = 0;
         uint32_t *claims = GOL_BYTES_PAIRED ? claim_counters(s, cus) : nullptr;
         if (strip <= 0 && cus > 0 &&
-            rank_split(rows, a.ngroups, cus, (int)(slots / cus), BYTES_PIPE_RANK_W, 2 * k, 1024, a.sm, claims, 4)) {
+            rank_split(rows, a.ngroups, cus, (int)std::min<int64_t>(GOL_BYTES_PER_CU, slots / cus), BYTES_PIPE_RANK_W,
+                       2 * k, 1024, a.sm, claims, 4)) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
             if (strip <= 0) {
