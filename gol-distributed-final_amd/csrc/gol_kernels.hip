@@ -1180,6 +1180,27 @@ __device__ __forceinline__ void lds_wait3(uint32_t (&r)[3])
 #ifndef GOL_BYTES_NS
 #define GOL_BYTES_NS 4
 #endif
+// Input ring of the byte pipeline's first wave: blocks of 3 byte rows staged HBM -> LDS with
+// global_load_lds (no VGPRs), NSI - 1 blocks in flight while the wave packs and computes one.
+#ifndef GOL_BYTES_NSI
+#define GOL_BYTES_NSI 4
+#endif
+// The six 16-byte halves of one input block (row S: lo at S * 2 KiB, hi at S * 2 KiB + 1 KiB,
+// lane * 16 within each), read and waited for together.
+__device__ __forceinline__ void lds_rd_block6(const lds_u32 *p, v4u32 (&r)[6])
+{
+    asm volatile(
+        "ds_read_b128 %0, %6\n\t"
+        "ds_read_b128 %1, %6 offset:1024\n\t"
+        "ds_read_b128 %2, %6 offset:2048\n\t"
+        "ds_read_b128 %3, %6 offset:3072\n\t"
+        "ds_read_b128 %4, %6 offset:4096\n\t"
+        "ds_read_b128 %5, %6 offset:5120\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5])
+        : "v"(p)
+        : "memory");
+}
 // 1-D grid of work items (work_item).  P waves of one column group: wave 0 loads its input
 // byte rows (one 3-row block ahead, in registers) and packs them with v_dot4_i32_i8, runs KF
 // stages and hands the block on; waves 1 .. P-2 run KM stages each; wave P-1 runs KL stages,
@@ -1194,8 +1215,10 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     constexpr int KX = KM > KF ? (KM > KL ? KM : KL) : (KF > KL ? KF : KL);
     static_assert(K <= 32, "one 32-cell halo word per side");
     constexpr int NS = GOL_BYTES_NS;
+    constexpr int NSI = GOL_BYTES_NSI;
     constexpr int ROW = 64;  // uint32 per LDS row
     __shared__ uint32_t ring[P - 1][NS][3][ROW];
+    __shared__ uint32_t in_ring[NSI][3][2][256];  // byte rows: [half][lane][16 bytes]
     __shared__ uint2 lut[256];
     __shared__ int ready[P], consumed[P];
     __shared__ int flag_scratch[P][64];  // flag writes of lanes 1..63 (see lds_flag_wr)
@@ -1228,13 +1251,18 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     // stream position t (input row index of this pipeline) -> input row / output row
     auto in_row = [&](int t) { return dir >= 0 ? first_in + t : s1e + K - 1 - t; };
     auto out_row = [&](int t) { return dir >= 0 ? s0 + t - 2 * K : s1e - 1 + 2 * K - t; };
-    auto load = [&](int t, Raw32 &r) {  // wave 0
-        int y = in_row(t);
-        y = y > last_in ? last_in : (y < first_in ? first_in : y);  // past the end: clamped, never stored
-        const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
-        const uint4 *q = reinterpret_cast<const uint4 *>(mid_b + (d + (int64_t)y * pitch) + lane_off);
-        r.lo = q[0];
-        r.hi = q[1];
+    // wave 0: block b -> an in_ring slot (the slot is an argument: a lambda that captures a
+    // __shared__ array loses the kernel's host-side stub)
+    auto stage_in = [&](int b, uint32_t (*slot)[2][256]) {
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+            int y = in_row(3 * b + S);
+            y = y > last_in ? last_in : (y < first_in ? first_in : y);  // past the end: clamped, never stored
+            const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
+            const char *g = mid_b + (d + (int64_t)y * pitch) + lane_off;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[S][0][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 16), &slot[S][1][0], 16, 0, 0);
+        }
     };
     for (int i = threadIdx.x; i < 256; i += 64 * P) {
         uint32_t o[2];
@@ -1248,6 +1276,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
     __syncthreads();
     lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
+    lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
     auto slot_row = [&](int e, int b, int S) {  // ring e (input of wave e), e >= 1
@@ -1271,7 +1300,6 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
         constexpr int ROLE = decltype(role_c)::value;  // 0 first, 1 middle, 2 last
         constexpr int NSTG = ROLE == 0 ? KF : (ROLE == 2 ? KL : KM);
         int seen_ready = 0, seen_free = 0;
-        Raw32 buf[3];
         int nb = nblk;        // role 0: blocks granted so far
         uint32_t next = 0;    // role 0, paired: blocks claimed before the pending claim
         if constexpr (ROLE == 0) {
@@ -1285,7 +1313,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                 if (nb == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);  // prefetched claim
             }
 #pragma unroll
-            for (int S = 0; S < 3; ++S) load(S, buf[S]);
+            for (int i = 0; i < NSI - 1; ++i) stage_in(i, in_ring[i]);
         }
         // Readers (waves 1 .. P-1): block b+1's rows are read at the end of block b (spinning
         // there for its flag if needed) and waited for at the top of block b+1; a middle wave
@@ -1315,10 +1343,16 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                     nb += g;
                     if (g == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);
                 }
+                // block b landed (blocks b+1 .. b+NSI-2 may still be in flight: 6 loads each)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSI - 2) * 6) : "memory");
+                v4u32 raw[6];
+                lds_rd_block6(in_l + (b % NSI) * (3 * 2 * 256) + lane * 4, raw);
 #pragma unroll
-                for (int S = 0; S < 3; ++S) w3[S] = pack32_ff(buf[S].lo, buf[S].hi);
-#pragma unroll
-                for (int S = 0; S < 3; ++S) load(3 * (b + 1) + S, buf[S]);  // clamped past the end
+                for (int S = 0; S < 3; ++S)
+                    w3[S] = pack32_ff(uint4{raw[2 * S].x, raw[2 * S].y, raw[2 * S].z, raw[2 * S].w},
+                                      uint4{raw[2 * S + 1].x, raw[2 * S + 1].y, raw[2 * S + 1].z, raw[2 * S + 1].w});
+                // refill block b-1's slot (read to completion in the previous trip; clamped past the end)
+                stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);
             } else {
                 if (!more) break;
                 lds_wait3(nx);  // block b's rows (and every older LDS operation of this wave)
@@ -1384,6 +1418,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     if (wv == 0) ok = run(std::integral_constant<int, 0>());
     else if (wv == P - 1) ok = run(std::integral_constant<int, 2>());
     else ok = run(std::integral_constant<int, 1>());
+    if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input blocks staged past the end
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
     if (a.slots && wv == P - 1) slot_add(a.slots, alive);
 }

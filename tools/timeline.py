@@ -21,7 +21,7 @@ OUT = os.path.join(ROOT, "tools", "tl")
 LIB = os.environ.get("GOL_TL_LIB") or os.path.join(ROOT, "tools", "tl", "libtimeline.so")
 
 ENTRY = "    const int lane = threadIdx.x & 63;\n"
-STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n"
+STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n    const uint64_t tl_c0 = __builtin_amdgcn_s_memtime(); (void)tl_c0;\n"
 EXIT_BAND = "    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
 EXIT_BYTES = "    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);\n    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
 STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear workgroup id * P + wave
@@ -32,7 +32,8 @@ STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear w
         if ((threadIdx.x & 63) == 0) {
             a.slots[4 * i] = tl_t0; a.slots[4 * i + 1] = tl_t1;
 #ifdef GOL_EXP_PROF
-            a.slots[4 * i + 2] = prof_a; a.slots[4 * i + 3] = prof_b; (void)hw; (void)xcc;
+            a.slots[4 * i] = tl_c0; a.slots[4 * i + 1] = __builtin_amdgcn_s_memtime();
+            a.slots[4 * i + 2] = prof_a; a.slots[4 * i + 3] = prof_b | ((uint64_t)wv << 56); (void)hw; (void)xcc;
 #else
             a.slots[4 * i + 2] = hw; a.slots[4 * i + 3] = xcc;
 #endif
@@ -46,6 +47,7 @@ PROF_SPINS = (  # -DGOL_EXP_PROF: cycles each wave spends in its flag waits (rea
     ("seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);", "prof_b"),
     ("seen_ready = spin_until_ge(ready_l + wv, b + 2);", "prof_a"),
     ("seen_ready = spin_until_ge(ready_l + wv, b + 1);", "prof_a"),
+    ("seen_ready = spin_until_ge(ready_l + wv, 1);", "prof_a"),
 )
 
 
@@ -54,7 +56,8 @@ def build(flags=""):
     src = open(os.path.join(CSRC, "gol_kernels.hip")).read()
     if "GOL_EXP_PROF" in flags:
         for stmt, acc in PROF_SPINS:
-            assert stmt in src, stmt
+            if stmt not in src:
+                continue
             src = src.replace(stmt, "{ const uint64_t pt_ = __builtin_amdgcn_s_memtime(); " + stmt +
                               f" {acc} += __builtin_amdgcn_s_memtime() - pt_; }}")
         for kern in ("band_pipe_kernel(BitsArgs a)", "bytes_pipe_kernel(BytesKArgs a)"):
@@ -142,6 +145,14 @@ def run(workload, strip):
            "cus_used": len(per_cu), "waves_per_cu": sorted({c for c, _ in per_cu.values()}),
            "cu_end_us_pct": [round(float(np.percentile([x for _, x in per_cu.values()], q)), 1) for q in (0, 10, 50, 90, 100)],
            "simd_hist": np.bincount(simd, minlength=4).tolist()}
+    if os.environ.get("GOL_TL_PROF"):  # prof build: slots = (c0, c1, ready-wait, free-wait | role << 56) in shader cycles
+        life_c = (v[:, 1] - v[:, 0]).astype(np.float64)
+        role = (v[:, 3] >> 56) & 0xFF
+        out["prof"] = {int(r): {"waves": int((role == r).sum()), "life_Mcyc_med": round(float(np.median(life_c[role == r])) / 1e6, 3),
+                                "ready_wait_frac": round(float(v[role == r, 2].sum() / life_c[role == r].sum()), 4),
+                                "free_wait_frac": round(float((v[role == r, 3] & ((1 << 56) - 1)).sum() / life_c[role == r].sum()), 4)}
+                       for r in np.unique(role)}
+        out["start_us_pct"] = out["end_us_pct"] = out["life_us_pct"] = None
     print(json.dumps(out))
     np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{workload}_{strip}.npy"), v)
 
