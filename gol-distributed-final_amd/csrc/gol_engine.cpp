@@ -811,6 +811,24 @@ extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
 // readPgmImage header (gol/io.go:97-117): fields = strings.Fields(data): "P5", width, height,
 // maxval; the raster is fields[4], i.e. it starts at the first non-space byte after maxval.
 static bool is_space(uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+// strconv.Atoi with its error dropped (io.go:104-116 `v, _ := strconv.Atoi(f)`): an optional sign
+// and ASCII digits; anything else gives 0, out of range gives the clamped int64.
+static int64_t go_atoi(const std::string &f)
+{
+    size_t i = (!f.empty() && (f[0] == '+' || f[0] == '-')) ? 1 : 0;
+    if (i == f.size()) return 0;
+    const bool neg = f[0] == '-';
+    uint64_t v = 0;
+    bool big = false;
+    for (size_t j = i; j < f.size(); ++j) {
+        if (f[j] < '0' || f[j] > '9') return 0;
+        const uint64_t d = (uint64_t)(f[j] - '0');
+        if (v > (UINT64_MAX - d) / 10) big = true;
+        else v = v * 10 + d;
+    }
+    if (big || v > (uint64_t)INT64_MAX + (neg ? 1 : 0)) return neg ? INT64_MIN : INT64_MAX;
+    return neg ? (int64_t)(0 - v) : (int64_t)v;
+}
 static int parse_pgm_header(const uint8_t *h, size_t n, int64_t W, int64_t H, int64_t *off)
 {
     std::string f[4];
@@ -826,9 +844,9 @@ static int parse_pgm_header(const uint8_t *h, size_t n, int64_t W, int64_t H, in
     }
     if (nf < 1 || f[0] != "P5") return gol_set_error(GOL_EFORMAT, "Not a pgm file");
     if (nf < 4) return gol_set_error(GOL_EFORMAT, "Not a pgm file");
-    if (atoll(f[1].c_str()) != W) return gol_set_error(GOL_EFORMAT, "Incorrect width");
-    if (atoll(f[2].c_str()) != H) return gol_set_error(GOL_EFORMAT, "Incorrect height");
-    if (atoll(f[3].c_str()) != 255) return gol_set_error(GOL_EFORMAT, "Incorrect maxval/bit depth");
+    if (go_atoi(f[1]) != W) return gol_set_error(GOL_EFORMAT, "Incorrect width");
+    if (go_atoi(f[2]) != H) return gol_set_error(GOL_EFORMAT, "Incorrect height");
+    if (go_atoi(f[3]) != 255) return gol_set_error(GOL_EFORMAT, "Incorrect maxval/bit depth");
     while (i < n && is_space(h[i])) ++i;
     if (i >= n) return gol_set_error(GOL_EFORMAT, "no pixel data after the header");
     *off = (int64_t)i;

@@ -12,6 +12,16 @@ from ._lib import GOL_EFORMAT, GolError
 _SPACE = b" \t\n\v\f\r"
 
 
+def go_atoi(field: bytes) -> int:
+    """strconv.Atoi with its error dropped (io.go:104-116): an optional sign and ASCII digits;
+    anything else is 0, out of range is the clamped int64."""
+    digits = field[1:] if field[:1] in (b"+", b"-") else field
+    if not digits or any(c < 0x30 or c > 0x39 for c in digits):
+        return 0
+    v = int(digits.decode("ascii")) * (-1 if field[:1] == b"-" else 1)
+    return max(-(1 << 63), min((1 << 63) - 1, v))
+
+
 def pgm_header(head: bytes, width: int | None = None, height: int | None = None) -> tuple[int, int, int]:
     """io.go:90-126 header rules on the first bytes of a P5 file: fields = strings.Fields(data);
     "P5", width, height, 255.  Returns (W, H, offset of the first raster byte)."""
@@ -27,10 +37,9 @@ def pgm_header(head: bytes, width: int | None = None, height: int | None = None)
         i = j
     if not fields or fields[0] != b"P5":
         raise GolError(GOL_EFORMAT, "Not a pgm file")
-    try:
-        W, H, maxval = int(fields[1]), int(fields[2]), int(fields[3])
-    except (IndexError, ValueError):
+    if len(fields) < 4:
         raise GolError(GOL_EFORMAT, "Not a pgm file")
+    W, H, maxval = go_atoi(fields[1]), go_atoi(fields[2]), go_atoi(fields[3])
     if width is not None and W != width:
         raise GolError(GOL_EFORMAT, "Incorrect width")
     if height is not None and H != height:
