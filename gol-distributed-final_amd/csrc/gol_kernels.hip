@@ -677,7 +677,9 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 // published into ring e, consumed[e] = blocks taken out of it; a producer fills slot b % 3
 // once block b-3 is consumed.  Every spin is bounded (spin_until_ge).  1-D grid of work items
 // (work_item).
-template <int KW, int P, bool CONTIG>
+// COUNT: the last wave adds the alive cells of the rows it stores to a.slots (branch-free: a
+// per-row uniform mask, no branch around the count as a null-slots check made it).
+template <int KW, int P, bool CONTIG, bool COUNT>
 __global__ void __launch_bounds__(64 * P)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
 band_pipe_kernel(BitsArgs a)
@@ -691,7 +693,7 @@ band_pipe_kernel(BitsArgs a)
     __shared__ uint32_t in_ring[NS][3][ROW];
     __shared__ uint32_t ring[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
     __shared__ int ready[P], consumed[P];
-    __shared__ int flag_scratch[P][64];
+    __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (never read; all waves share it)
 
     const int lane = threadIdx.x & 63;
     int group, s0, s1, rotv;
@@ -771,7 +773,7 @@ band_pipe_kernel(BitsArgs a)
     //    their stores fall outside the strip's buffer range.
     const int nblk3 = (nblk + 2) / 3 * 3;
     constexpr int SB = SLOT * 4, RB = ROW * 4;  // slot and row strides in bytes
-    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0][0] + wv * 64 + lane;
+    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
     lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // writer: ring wv+1 ready
     lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // reader: ring wv consumed
     lds_u32 *const in_base = in_l + lane * 4;
@@ -808,8 +810,10 @@ band_pipe_kernel(BitsArgs a)
         __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, 2);
         // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are masked
         // once at the end)
-        if (a.slots && (uint32_t)rrel < nrows)
-            alive += __popc(cur[0]) + __popc(cur[1]) + __popc(cur[2]) + __popc(cur[3]);
+        if constexpr (COUNT) {
+            const uint32_t m = (uint32_t)rrel < nrows ? 0xFFFFFFFFu : 0u;
+            alive += (__popc(cur[0]) + __popc(cur[1]) + __popc(cur[2]) + __popc(cur[3])) & m;
+        }
         voff += vstep;
         rrel += rstep;
     };
@@ -939,7 +943,7 @@ band_pipe_kernel(BitsArgs a)
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
     alive &= st_mask;  // halo lanes' rows are not this group's
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (a.slots && wv == P - 1) slot_add(a.slots, alive);
+    if (COUNT && wv == P - 1) slot_add(a.slots, alive);
 }
 
 // 32 x 32 bit-matrix transpose in registers: afterwards x[i] bit b = (before) x[b] bit i.
@@ -1173,17 +1177,22 @@ __device__ __forceinline__ void lds_wait3(uint32_t (&r)[3])
 #define GOL_BYTES_PER_CU 3  // workgroups per CU of a one-round launch
 #endif
 // Ring slots per inter-wave ring of the byte pipeline: 4 measured +1.5 % over 3 (16384^2, same
-// box); with the hand-off software-pipelined (reads one block ahead, no wait for own writes)
+// box), 6 (with NSI = 3 below, which alone cost 0.6 %, and one flag-scratch row for all waves:
+// 53 KiB per workgroup, still 3 per CU) +1.3-3 % over 4; role order reversed on each SIMD (the
+// older wave of a SIMD the downstream one) -5 %; with the hand-off software-pipelined (reads one block ahead, no wait for own writes)
 // the byte pipeline ran within 2 % of the blocking version, and 4 x 8-stage waves equal to 8 x 4:
 // at ~0.45-0.49 of the VALU issue roof neither the hand-off nor the HBM streams (no loads and
 // no stores: +10 %) bound it.
 #ifndef GOL_BYTES_NS
-#define GOL_BYTES_NS 4
+#define GOL_BYTES_NS 6
 #endif
 // Input ring of the byte pipeline's first wave: blocks of 3 byte rows staged HBM -> LDS with
 // global_load_lds (no VGPRs), NSI - 1 blocks in flight while the wave packs and computes one.
 #ifndef GOL_BYTES_NSI
-#define GOL_BYTES_NSI 4
+#define GOL_BYTES_NSI 3
+#endif
+#ifndef GOL_BYTES_ROLE_SHIFT
+#define GOL_BYTES_ROLE_SHIFT 0
 #endif
 // The six 16-byte halves of one input block (row S: lo at S * 2 KiB, hi at S * 2 KiB + 1 KiB,
 // lane * 16 within each), read and waited for together.
@@ -1221,10 +1230,10 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     __shared__ uint32_t in_ring[NSI][3][2][256];  // byte rows: [half][lane][16 bytes]
     __shared__ uint2 lut[256];
     __shared__ int ready[P], consumed[P];
-    __shared__ int flag_scratch[P][64];  // flag writes of lanes 1..63 (see lds_flag_wr)
+    __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (lds_flag_wr; never read)
 
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + GOL_BYTES_ROLE_SHIFT) % P);
     int group, s0, s1, rotv;
     if (!work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv)) return;
     uint32_t *ctr;
@@ -1282,7 +1291,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     auto slot_row = [&](int e, int b, int S) {  // ring e (input of wave e), e >= 1
         return ring_l + (((e - 1) * NS + b % NS) * 3 + S) * ROW + lane;
     };
-    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0][0] + wv * 64 + lane;
+    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
     lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // ring wv+1 ready
     lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // ring wv consumed
 
@@ -2032,7 +2041,9 @@ static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
     constexpr int KW = 3, P = 4;
-    const void *kf = contig ? (const void *)band_pipe_kernel<KW, P, true> : (const void *)band_pipe_kernel<KW, P, false>;
+    const bool count = a.slots != nullptr;
+    const void *kf = contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true> : (const void *)band_pipe_kernel<KW, P, true, false>)
+                            : (count ? (const void *)band_pipe_kernel<KW, P, false, true> : (const void *)band_pipe_kernel<KW, P, false, false>);
     int64_t nwg = 0;
     const int cus = device_cus();
     const int64_t slots = resident_workgroups(kf, 64 * P);
@@ -2056,10 +2067,14 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
             nwg = a.sm.tail_l + a.ngroups * ((tail_rows + ts - 1) / ts);
         }
     }
-    if (contig)
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
+    if (contig && count)
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
+    else if (contig)
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
+    else if (count)
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
     else
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false>), dim3((unsigned)nwg), dim3(64 * P), 0, s, a);
     return hipGetLastError();
 }
 

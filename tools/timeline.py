@@ -22,7 +22,7 @@ LIB = os.environ.get("GOL_TL_LIB") or os.path.join(ROOT, "tools", "tl", "libtime
 
 ENTRY = "    const int lane = threadIdx.x & 63;\n"
 STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n    const uint64_t tl_c0 = __builtin_amdgcn_s_memtime(); (void)tl_c0;\n"
-EXIT_BAND = "    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
+EXIT_BAND = "    if (COUNT && wv == P - 1) slot_add(a.slots, alive);\n}"
 EXIT_BYTES = "    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);\n    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
 STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear workgroup id * P + wave
         const uint64_t tl_t1 = __builtin_amdgcn_s_memrealtime();
@@ -69,7 +69,8 @@ def build(flags=""):
         j = src.index(ENTRY, i)
         src = src[:j] + STAMP_T0 + src[j + len(ENTRY):]
         k = src.index(exit_, j)
-        src = src[:k] + exit_.replace("    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}", STORE) + src[k + len(exit_):]
+        count_line = exit_[exit_.rindex("    if ("):]  # the kernel's final slot_add (and closing brace)
+        src = src[:k] + exit_.replace(count_line, STORE) + src[k + len(exit_):]
     open(os.path.join(OUT, "gol_kernels.hip"), "w").write(src)
     for f in os.listdir(CSRC):
         if f.endswith((".cpp", ".h")) or f == "Makefile":

@@ -5,10 +5,10 @@
 #include "gol_kernels.hip"
 
 template <int KW, int MODE>
-__global__ void __launch_bounds__(512) bs_kernel(uint32_t *out, uint64_t *cyc, int iters)
+__global__ void __launch_bounds__(256) bs_kernel(uint32_t *out, uint64_t *cyc, int iters)
 {
     using namespace golk;
-    __shared__ uint32_t slot[8][3][64];
+    __shared__ uint32_t slot[4][3][64];
     lds_u32 *const my = (lds_u32 *)&slot[threadIdx.x >> 6][0][0] + (threadIdx.x & 63);
     Pipe<KW, 1> p;
     pipe_init(p);
@@ -38,11 +38,11 @@ __global__ void __launch_bounds__(512) bs_kernel(uint32_t *out, uint64_t *cyc, i
 template <int KW, int MODE>
 void run(int wps)
 {
-    const int blocks = 256, threads = 64 * 4 * wps, iters = 4000;  // one workgroup per CU
+    const int blocks = 256 * wps, threads = 256, iters = 4000;  // wps workgroups of 4 waves per CU
     uint32_t *out;
     uint64_t *cyc;
     (void)hipMalloc(&out, (size_t)blocks * threads * 4);
-    (void)hipMalloc(&cyc, (size_t)blocks * 32 * 8);
+    (void)hipMalloc(&cyc, (size_t)blocks * 4 * 8);
     hipLaunchKernelGGL((bs_kernel<KW, MODE>), dim3(blocks), dim3(threads), 0, 0, out, cyc, 10);
     hipLaunchKernelGGL((bs_kernel<KW, MODE>), dim3(blocks), dim3(threads), 0, 0, out, cyc, iters);
     (void)hipDeviceSynchronize();

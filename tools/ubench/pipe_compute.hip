@@ -4,6 +4,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -I../../include -I../../gol-distributed-final_amd/csrc pipe_compute.hip -o pipe_compute
 #include "gol_kernels.hip"
 
+// MODE bit 2 (4): the op-by-op stage (bstage) instead of the word-by-word one (bstage_seq).
 // MODE 0: compute only.  MODE 1: + the pipe kernel's LDS hand-off per row (ds_write_b128 of
 // the row's result, ds_read_b128 of the next row issued one row ahead, waited with
 // lgkmcnt(1)), on the wave's own slot so there is no cross-wave waiting.  MODE 2: + one
@@ -40,9 +41,15 @@ __global__ void __launch_bounds__(256) pc_kernel(uint32_t *out, uint64_t *cyc, i
             }
 #pragma unroll
             for (int g = 0; g < KW; ++g) {
-                if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
-                if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
-                if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+                if (MODE & 4) {
+                    if (S == 0) bstage<KW, DW, 0>(p, g, cur);
+                    if (S == 1) bstage<KW, DW, 1>(p, g, cur);
+                    if (S == 2) bstage<KW, DW, 2>(p, g, cur);
+                } else {
+                    if (S == 0) bstage_seq<KW, DW, 0>(p, g, cur);
+                    if (S == 1) bstage_seq<KW, DW, 1>(p, g, cur);
+                    if (S == 2) bstage_seq<KW, DW, 2>(p, g, cur);
+                }
             }
 #pragma unroll
             for (int j = 0; j < DW; ++j) acc ^= cur[j];
@@ -89,11 +96,12 @@ void run(int wps)
 int main()
 {
     for (int rep = 0; rep < 2; ++rep)
-        for (int w : {2, 4}) {
+        for (int w : {1, 2, 3, 4}) {
             run<3, 0>(w);
+            run<3, 4>(w);
             run<3, 1>(w);
-            run<3, 2>(w);
             run<3, 3>(w);
+            run<3, 7>(w);
         }
     return 0;
 }
