@@ -1191,9 +1191,6 @@ __device__ __forceinline__ void lds_wait3(uint32_t (&r)[3])
 #ifndef GOL_BYTES_NSI
 #define GOL_BYTES_NSI 3
 #endif
-#ifndef GOL_BYTES_ROLE_SHIFT
-#define GOL_BYTES_ROLE_SHIFT 0
-#endif
 // The six 16-byte halves of one input block (row S: lo at S * 2 KiB, hi at S * 2 KiB + 1 KiB,
 // lane * 16 within each), read and waited for together.
 __device__ __forceinline__ void lds_rd_block6(const lds_u32 *p, v4u32 (&r)[6])
@@ -1233,7 +1230,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (lds_flag_wr; never read)
 
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + GOL_BYTES_ROLE_SHIFT) % P);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int group, s0, s1, rotv;
     if (!work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv)) return;
     uint32_t *ctr;
