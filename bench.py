@@ -117,6 +117,9 @@ class Ranks:
             assert dist.get_world_size() == args.gpus
             self.dist = dist
         self.dry = args.dry_run
+        if not self.dry:
+            import torch
+            torch.cuda.set_device(self.local)  # barrier()'s synchronize is then this rank's GPU
 
     def barrier(self):
         if self.dist is not None:

@@ -62,6 +62,40 @@ def test_loopback_shards_vs_oracle(G, n, H, W, layout):
         assert e.alive_count() == O.popcount_words(ref)
 
 
+@pytest.mark.parametrize("H,n,W,layout", [(9, 4, 1024, "band"), (5, 3, 2048, "band"), (4, 4, 1024, "band"),
+                                           (7, 3, 128, "standard"), (3, 3, 64, "standard")])
+def test_tiny_shards_cap_turns_per_launch(G, H, n, W, layout):
+    """Shards of 1-3 rows: the engine caps k at the smallest shard (the halo exchange hands over
+    k rows of ONE neighbour), so every launch is exact; 29 turns against the oracle."""
+    seed = 100 + H * n
+    words = O.random_words(seed, 0, H, W // 64)
+    ref, counts = O.bits_run(words, 29, with_counts=True)
+    with _sharded(G, H, W, n, layout=layout) as e:
+        assert [e.shard(i)["y1"] - e.shard(i)["y0"] for i in range(n)] == \
+            [O.partition(H, n, i)[1] - O.partition(H, n, i)[0] for i in range(n)]
+        e.load_random(seed)
+        assert e.step_counted(29, 1).tolist() == list(counts[:29])
+        assert e.hash() == O.hash_words(ref)
+
+
+@pytest.mark.parametrize("H,W", [(16, 16), (33, 32), (20, 48), (9, 8)])
+def test_narrow_boards_byte_path(G, H, W):
+    """Widths below 64 (or not a multiple of 64) run on the exact byte board: vs the literal port."""
+    rng = np.random.default_rng(H * W)
+    board = (rng.random((H, W)) < 0.4).astype(np.uint8) * 255
+    with G.Engine(H, W, device=0) as e:
+        e.load_bytes(board)
+        counts = e.step_counted(23, 1)
+        got = e.store_bytes()
+    ref = board
+    want = []
+    for _ in range(23):
+        ref = O.run(ref, 1)
+        want.append(int(np.count_nonzero(ref)))
+    assert np.array_equal(got, ref)
+    assert counts.tolist() == want
+
+
 @pytest.mark.parametrize("n", [2, 3])
 def test_shards_bytes_golden_alive_list_pgm(G, golden_dir, tmp_path, n):
     """TestGol / TestPgm on the 512x512 golden board through a sharded engine: alive list in
