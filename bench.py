@@ -56,6 +56,8 @@ def parse(argv=None):
                          "(12 band / 8 standard), 32 for byte16k")
     ap.add_argument("--strip", type=int, default=0, help="rows per strip (0 = auto)")
     ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"])
+    ap.add_argument("--cpl", type=int, default=0, choices=[0, 32, 64, 128],
+                    help="cells per lane of the bit kernels (0 = library default: 128 on the band layout)")
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -255,7 +257,8 @@ def run_bits(args, ranks):
     if args.share_gpu and sharded and world > 1:
         # test mode: every rank an independent 1-GPU replica of rows_per_gpu rows
         H, sharded = H // world, False
-    kw = dict(device=ranks.local, turns_per_launch=args.k, strip_rows=args.strip, layout=args.layout)
+    kw = dict(device=ranks.local, turns_per_launch=args.k, strip_rows=args.strip, layout=args.layout,
+              cells_per_lane=args.cpl)
     if sharded and world > 1:
         uid = ranks.share(golhip.engine.rccl_unique_id() if rank == 0 else None)
         e = golhip.Engine.rank(H, W, world, rank, uid, **kw)
@@ -295,6 +298,8 @@ def run_bits(args, ranks):
                 "note": "device unpack + D2H + pwrite of every rank's rows (PCIe and disk inclusive)"}
     layout = {0: "bytes", 1: "standard", 2: "band"}[2 if info["layout"] == "band" else 1]
     key = f"{args.workload}:{args.rows_per_gpu if args.workload == 'weak' else H}x{W}:k{k}:{layout}"
+    if info["cells_per_lane"] != 128:
+        key += f":cpl{info['cells_per_lane']}"
     pmc, note = load_pmc(key)
     roof = roofline("bits", t["mean_ms"], t["mean_cell_updates"], pmc, note)
     rpg = args.rows_per_gpu

@@ -52,14 +52,14 @@ static int set_dev(int d)
 }
 
 // Turns per launch: the largest supported k <= want, the remaining turns and the smallest
-// shard.  k = 12 is the band layout's split pipeline (4 words per lane); k = 16 needs <= 2
-// words per lane.
+// shard.  k = 12 is the band layout's (the split pipeline at 4 words per lane, one wave for
+// all 12 turns at 2); k = 16 needs <= 2 words per lane.
 static int pick_k(int want, int64_t remaining, int64_t rows, int dw, bool band)
 {
     static const int ks[] = {16, 12, 8, 4, 2, 1};
     for (int k : ks) {
         if (k == 16 && dw > 2) continue;
-        if (k == 12 && !(band && dw == 4)) continue;
+        if (k == 12 && !band) continue;  // band: the split pipeline (4 words per lane) or one wave (2)
         if (k <= want && k <= remaining && k <= rows) return k;
     }
     return 1;

@@ -1894,6 +1894,8 @@ static hipError_t launch_band(int k, dim3 grid, const BitsArgs &a, hipStream_t s
     case 2: hipLaunchKernelGGL((band_step_kernel<2, DW, C>), grid, dim3(256), 0, s, a); break;
     case 4: hipLaunchKernelGGL((band_step_kernel<4, DW, C>), grid, dim3(256), 0, s, a); break;
     case 8: hipLaunchKernelGGL((band_step_kernel<8, DW, C>), grid, dim3(256), 0, s, a); break;
+    case 12: if constexpr (DW <= 2) { hipLaunchKernelGGL((band_step_kernel<12, DW, C>), grid, dim3(256), 0, s, a); break; }
+             return hipErrorInvalidValue;
     case 16: if constexpr (DW <= 2) { hipLaunchKernelGGL((band_step_kernel<16, DW, C>), grid, dim3(256), 0, s, a); break; }
              return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;

@@ -142,7 +142,7 @@ def test_kernel_variants_vs_bit_oracle(golhip, k, cpl):
 
 
 @pytest.mark.parametrize("k,cpl", [(1, 128), (2, 128), (4, 128), (8, 128), (12, 128), (1, 64), (4, 64), (8, 64),
-                                   (16, 64)])
+                                   (12, 64), (16, 64)])
 @pytest.mark.parametrize("shape", [(300, 1024), (97, 2048), (64, 3072), (33, 8192), (5, 1024)])
 def test_band_layout_vs_bit_oracle(golhip, k, cpl, shape):
     """Band-layout kernel (bit b of word w = cell b*W/32 + w) for every (k, words per lane):
@@ -157,7 +157,7 @@ def test_band_layout_vs_bit_oracle(golhip, k, cpl, shape):
         assert info["layout"] == "band" and info["cells_per_lane"] == cpl
         assert info["turns_per_launch"] == min(k, 16 if H >= 16 else 4 if H >= 4 else 1)
         if k == 12:
-            assert info["turns_per_launch"] in (12, 4)  # the split pipeline (4 waves x 3 turns)
+            assert info["turns_per_launch"] in (12, 4)  # split pipeline (4 waves x 3 turns) / one wave at 64 cpl
         e.step(20)
         assert e.alive_count() == counts[19]  # popcount on the band layout
         e.step(25)
