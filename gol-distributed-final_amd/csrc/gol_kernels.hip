@@ -33,6 +33,12 @@
 #ifndef GOL_SPIN_LIMIT
 #define GOL_SPIN_LIMIT (1 << 22)
 #endif
+// s_sleep argument between two polls of a pipeline flag (units of 64 shader cycles): 0 (the
+// poll's own LDS round trip paces it) measured +1 % on 65536^2, +0.3 % on 16384^2 bytes, equal on
+// the weak board, over 1; 2 was slower (same box, tools/ab.py)
+#ifndef GOL_SPIN_SLEEP
+#define GOL_SPIN_SLEEP 0
+#endif
 
 namespace golk {
 
@@ -663,7 +669,7 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
     for (int n = 0; n < GOL_SPIN_LIMIT; ++n) {
         const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
         if (x >= v) return x;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
     }
     return -1;
 }
