@@ -1291,9 +1291,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
-    auto slot_row = [&](int e, int b, int S) {  // ring e (input of wave e), e >= 1
-        return ring_l + (((e - 1) * NS + b % NS) * 3 + S) * ROW + lane;
+    auto slot_row = [&](int e, int sl, int S) {  // ring e (input of wave e), e >= 1, slot sl
+        return ring_l + (((e - 1) * NS + sl) * 3 + S) * ROW + lane;
     };
+    // ring slots advance by one per block: running indices instead of b % NS (a division by a
+    // constant, ~6 scalar instructions per use)
+    auto next_slot = [](int x, int n) { return x + 1 == n ? 0 : x + 1; };
     lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
     lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // ring wv+1 ready
     lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // ring wv consumed
@@ -1344,7 +1347,8 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
             if (more) lds_rd32x3_issue(slot_row(wv, 0, 0), nx);
         }
         int b = 0;
-        for (;; ++b) {
+        int wsl = 0, rsl = 1 % NS, isl = 0;  // b % NS, (b + 1) % NS, b % NSI
+        for (;; ++b, wsl = next_slot(wsl, NS), rsl = next_slot(rsl, NS), isl = next_slot(isl, NSI)) {
             uint32_t w3[3];
             if constexpr (ROLE == 0) {
                 if (b >= nb) {
@@ -1358,13 +1362,13 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                 // block b landed (blocks b+1 .. b+NSI-2 may still be in flight: 6 loads each)
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSI - 2) * 6) : "memory");
                 v4u32 raw[6];
-                lds_rd_block6(in_l + (b % NSI) * (3 * 2 * 256) + lane * 4, raw);
+                lds_rd_block6(in_l + isl * (3 * 2 * 256) + lane * 4, raw);
 #pragma unroll
                 for (int S = 0; S < 3; ++S)
                     w3[S] = pack32_ff(uint4{raw[2 * S].x, raw[2 * S].y, raw[2 * S].z, raw[2 * S].w},
                                       uint4{raw[2 * S + 1].x, raw[2 * S + 1].y, raw[2 * S + 1].z, raw[2 * S + 1].w});
                 // refill block b-1's slot (read to completion in the previous trip; clamped past the end)
-                stage_in(b + NSI - 1, in_ring[(b + NSI - 1) % NSI]);
+                stage_in(b + NSI - 1, in_ring[isl == 0 ? NSI - 1 : isl - 1]);
             } else {
                 if (!more) break;
                 lds_wait3(nx);  // block b's rows (and every older LDS operation of this wave)
@@ -1399,7 +1403,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                     if (seen_free < 0) return false;
                 }
 #pragma unroll
-                for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, b, S), (int)w3[S]);
+                for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, wsl, S), (int)w3[S]);
             }
             if constexpr (ROLE != 0) {
                 if (seen_ready < b + 2) {
@@ -1407,7 +1411,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                     if (seen_ready < 0) return false;
                 }
                 more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
-                if (more) lds_rd32x3_issue(slot_row(wv, b + 1, 0), nx);
+                if (more) lds_rd32x3_issue(slot_row(wv, rsl, 0), nx);
             }
         }
         if constexpr (ROLE != 2) {
