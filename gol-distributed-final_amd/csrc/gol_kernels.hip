@@ -1220,7 +1220,7 @@ __device__ __forceinline__ void lds_rd_block6(const lds_u32 *p, v4u32 (&r)[6])
 // and stores.  The first and last waves carry the byte conversion, so they get fewer stages
 // (a wave that is busy when its consumer wants the next block sets the pipeline's rate).
 // One loop per role (no role branches inside the loop).
-template <int KF, int KM, int KL, int P>
+template <int KF, int KM, int KL, int P, bool COUNT>
 __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 {
     constexpr int K = KF + (P - 2) * KM + KL;
@@ -1256,7 +1256,6 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const int64_t bot_d = (reinterpret_cast<const char *>(a.bot) - mid_b) - (int64_t)R * pitch;
     const uint32_t lane_off = (uint32_t)(col * 32);
     char *dst_b = reinterpret_cast<char *>(a.dst);
-    const uint32_t row_bytes = (uint32_t)a.Wd * 32u;
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
 
@@ -1305,6 +1304,16 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     pipe_init(p);
     uint32_t alive = 0;
     const uint32_t nrows = (uint32_t)(s1 - s0);
+    // last wave: output row y = out_row(t) stored at voffset st_off + (y - s0) * pitch of ONE
+    // buffer spanning the strip's rows (the host keeps rows x pitch < 2^31): rows before s0
+    // (negative offsets, as unsigned >= 2^32 - 2K * pitch), from s1 on, and a halo lane's 2^31
+    // fall outside it, so no per-row descriptor or branch (as in band_pipe_kernel)
+    const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
+        dst_b + (int64_t)s0 * pitch, (short)0, (int)(nrows * (uint32_t)pitch), 0x00020000);
+    int rrel = out_row(0) - s0;  // output row - s0 of stream position 3b + S (wave-uniform)
+    const int rstep = dir >= 0 ? 1 : -1;
+    uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch;
+    const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch;
     // ready flags count published blocks; the first wave ends the stream with FINAL | blocks,
     // which every wave passes on after its last block (a paired pipeline learns its block count
     // only when a claim fails)
@@ -1378,20 +1387,26 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
             }
             sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
             if constexpr (ROLE == 2) {
+                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit takes
+                // its shift mod 32), unpack row by row through the LUT (all 12 reads ahead of the
+                // stores measured 0.9 % slower)
+                uint32_t o[3];
+                uint2 e[3][4];
 #pragma unroll
                 for (int S = 0; S < 3; ++S) {
-                    // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit
-                    // takes its shift mod 32)
                     const uint32_t nxw = from_upper_lane(w3[S]);
-                    const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nxw, w3[S], K % 32) : nxw;
-                    const uint2 e0 = lut[o & 0xFF], e1 = lut[(o >> 8) & 0xFF], e2 = lut[(o >> 16) & 0xFF], e3 = lut[o >> 24];
-                    const int y = out_row(3 * b + S);
-                    const bool row_ok = (uint32_t)(y - s0) < nrows;
-                    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                        dst_b + (int64_t)(row_ok ? y : s0) * pitch, (short)0, (int)(row_ok ? row_bytes : 0u), 0x00020000);
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e0.x, e0.y, e1.x, e1.y}, r, st_off, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e2.x, e2.y, e3.x, e3.y}, r, st_off + 16u, 0, 0);
-                    if (a.slots) alive += bitop3<0x80>((uint32_t)__popc(o), st_mask, row_ok ? 0xFFFFFFFFu : 0u);
+                    o[S] = K % 32 ? __builtin_amdgcn_alignbit(nxw, w3[S], K % 32) : nxw;
+                }
+#pragma unroll
+                for (int S = 0; S < 3; ++S) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) e[S][q] = lut[(o[S] >> (8 * q)) & 0xFF];
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[S][0].x, e[S][0].y, e[S][1].x, e[S][1].y}, strip_rs, voff, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[S][2].x, e[S][2].y, e[S][3].x, e[S][3].y}, strip_rs, voff + 16u, 0, 0);
+                    if constexpr (COUNT)
+                        alive += bitop3<0x80>((uint32_t)__popc(o[S]), st_mask, (uint32_t)rrel < nrows ? 0xFFFFFFFFu : 0u);
+                    voff += vstep;
+                    rrel += rstep;
                 }
             } else {
                 if constexpr (ROLE == 0) {
@@ -1436,7 +1451,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     else ok = run(std::integral_constant<int, 1>());
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input blocks staged past the end
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
-    if (a.slots && wv == P - 1) slot_add(a.slots, alive);
+    if (COUNT && wv == P - 1) slot_add(a.slots, alive);
 }
 
 // ------------------------------------------------------------------ byte-board step (exact semantics)
@@ -2043,7 +2058,7 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 #define GOL_BYTES_PIPE_STAGES 4, 4, 4
 #define GOL_BYTES_PIPE_P 8
 #endif
-#define BYTES_PIPE (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P>)
+#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
 static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
 
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
@@ -2175,23 +2190,29 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
     if (k == 32) {
         // one workgroup of GOL_BYTES_PIPE_P waves per (column group, strip): rank-weighted strips
         // in one round, else round-tiled strips >= 4k rows
-        const void *kf = (const void *)BYTES_PIPE;
+        const bool count = a.slots != nullptr;
+        const void *kf = count ? (const void *)BYTES_PIPE(true) : (const void *)BYTES_PIPE(false);
         const int cus = device_cus();
         const int64_t slots = resident_workgroups(kf, 64 * BYTES_PIPE_P);
         int64_t nwg = 0;
         uint32_t *claims = GOL_BYTES_PAIRED ? claim_counters(s, cus) : nullptr;
+        // the last wave stores a strip through one buffer descriptor: strip rows x pitch < 2^31
+        const int64_t max_rows = std::max<int64_t>(1, ((int64_t(1) << 31) - 1) / pitch - 1);
         if (strip <= 0 && cus > 0 &&
             rank_split(rows, a.ngroups, cus, (int)std::min<int64_t>(GOL_BYTES_PER_CU, slots / cus), BYTES_PIPE_RANK_W,
-                       2 * k, 1024, a.sm, claims, 4)) {
+                       2 * k, 1024, a.sm, claims, 4) && a.sm.period <= max_rows) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
+            a.sm = StripMap{};
             if (strip <= 0) {
                 a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, rows * a.ngroups / 1024));
                 a.strip = (int)round_tiled_strip(rows, a.ngroups, slots, 4 * k, 1024, a.strip);
             }
+            a.strip = (int)std::min<int64_t>(a.strip, max_rows);
             nwg = (int64_t)a.ngroups * ((rows + a.strip - 1) / a.strip);
         }
-        hipLaunchKernelGGL(BYTES_PIPE, dim3((unsigned)nwg), dim3(64 * BYTES_PIPE_P), 0, s, a);
+        if (count) hipLaunchKernelGGL(BYTES_PIPE(true), dim3((unsigned)nwg), dim3(64 * BYTES_PIPE_P), 0, s, a);
+        else hipLaunchKernelGGL(BYTES_PIPE(false), dim3((unsigned)nwg), dim3(64 * BYTES_PIPE_P), 0, s, a);
         return hipGetLastError();
     }
     const int nstrips = (int)((rows + a.strip - 1) / a.strip);
