@@ -665,13 +665,20 @@ __device__ __forceinline__ void lds_wr32(lds_u32 *p, int v) { asm volatile("ds_w
 // failed (GOL_EHIP) instead of returning a board with unwritten strips.
 __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 {
+#ifdef GOL_EXP_SPIN_PRIO
+    __builtin_amdgcn_s_setprio(0);  // a polling wave yields issue to the computing ones (prio 1)
+#endif
+    int r = -1;
 #pragma clang loop unroll(disable)
     for (int n = 0; n < GOL_SPIN_LIMIT; ++n) {
         const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
-        if (x >= v) return x;
+        if (x >= v) { r = x; break; }
         __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
     }
-    return -1;
+#ifdef GOL_EXP_SPIN_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+    return r;
 }
 
 // ------------------------------------------------------------------ band layout, split pipeline
@@ -750,6 +757,9 @@ band_pipe_kernel(BitsArgs a)
     };
 
     if (!has_rows) return;  // whole workgroup (no barrier after this point)
+#ifdef GOL_EXP_SPIN_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
     __syncthreads();
     lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
@@ -1275,6 +1285,9 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 16), &slot[S][1][0], 16, 0, 0);
         }
     };
+#ifdef GOL_EXP_SPIN_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     for (int i = threadIdx.x; i < 256; i += 64 * P) {
         uint32_t o[2];
 #pragma unroll
