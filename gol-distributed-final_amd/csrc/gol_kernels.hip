@@ -663,11 +663,13 @@ __device__ __forceinline__ void lds_wr32(lds_u32 *p, int v) { asm volatile("ds_w
 // each records GOLK_ERR_SPIN in the launch's error word on its way out (once, after the loop:
 // an atomic inside the loop costs the pipeline registers), so the host reports the launch as
 // failed (GOL_EHIP) instead of returning a board with unwritten strips.
+// YIELD (the byte pipeline, whose waves run at priority 1): the polling wave drops to priority 0,
+// so the computing waves of its SIMD win the issue arbitration (+1.5 % on 16384^2 bytes; the band
+// pipeline measured 0 / -1 %, same box).
+template <bool YIELD = false>
 __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 {
-#ifdef GOL_EXP_SPIN_PRIO
-    __builtin_amdgcn_s_setprio(0);  // a polling wave yields issue to the computing ones (prio 1)
-#endif
+    if constexpr (YIELD) __builtin_amdgcn_s_setprio(0);
     int r = -1;
 #pragma clang loop unroll(disable)
     for (int n = 0; n < GOL_SPIN_LIMIT; ++n) {
@@ -675,9 +677,7 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
         if (x >= v) { r = x; break; }
         __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
     }
-#ifdef GOL_EXP_SPIN_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
+    if constexpr (YIELD) __builtin_amdgcn_s_setprio(1);
     return r;
 }
 
@@ -757,9 +757,6 @@ band_pipe_kernel(BitsArgs a)
     };
 
     if (!has_rows) return;  // whole workgroup (no barrier after this point)
-#ifdef GOL_EXP_SPIN_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
     if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
     __syncthreads();
     lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
@@ -1285,9 +1282,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 16), &slot[S][1][0], 16, 0, 0);
         }
     };
-#ifdef GOL_EXP_SPIN_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
+    __builtin_amdgcn_s_setprio(1);  // polls drop to 0 (spin_until_ge<true>)
     for (int i = threadIdx.x; i < 256; i += 64 * P) {
         uint32_t o[2];
 #pragma unroll
@@ -1362,7 +1357,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
         bool more = true;
         if constexpr (ROLE != 0) {
             if (seen_ready < 1) {
-                seen_ready = spin_until_ge(ready_l + wv, 1);
+                seen_ready = spin_until_ge<true>(ready_l + wv, 1);
                 if (seen_ready < 0) return false;
             }
             more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
@@ -1427,7 +1422,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                     lds_flag_wr(rdy_addr, b);
                 }
                 if (seen_free < b + 1 - NS) {
-                    seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                    seen_free = spin_until_ge<true>(consumed_l + wv + 1, b + 1 - NS);
                     if (seen_free < 0) return false;
                 }
 #pragma unroll
@@ -1435,7 +1430,7 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
             }
             if constexpr (ROLE != 0) {
                 if (seen_ready < b + 2) {
-                    seen_ready = spin_until_ge(ready_l + wv, b + 2);
+                    seen_ready = spin_until_ge<true>(ready_l + wv, b + 2);
                     if (seen_ready < 0) return false;
                 }
                 more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
