@@ -1365,6 +1365,8 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
         }
         int b = 0;
         int wsl = 0, rsl = 1 % NS, isl = 0;  // b % NS, (b + 1) % NS, b % NSI
+        const int g0 = ROLE == 0 ? 0 : (ROLE == 2 ? K - KL : KF + (wv - 1) * KM);  // first stage of this wave
+        const int skip_b = (2 * g0) / 3;  // blocks 0 .. skip_b-1 end before step 2 g0
         for (;; ++b, wsl = next_slot(wsl, NS), rsl = next_slot(rsl, NS), isl = next_slot(isl, NSI)) {
             uint32_t w3[3];
             if constexpr (ROLE == 0) {
@@ -1393,7 +1395,11 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
                 lds_flag_wr(cns_addr, b + 1);
                 if constexpr (ROLE == 1) lds_flag_wr(rdy_addr, b);  // blocks < b: written and complete
             }
-            sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
+            // Fill rows: stage g's input is valid from stream step 2g on (each stage needs the two
+            // rows before), and only its outputs from step 2g + 2 on are ever used, so a wave whose
+            // first stage is g0 skips the blocks that end before step 2 g0 (their rows pass on as
+            // they are; its pipe state is stale until step 2 g0, where nothing needs it yet).
+            if (b >= skip_b) sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
             if constexpr (ROLE == 2) {
                 // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit takes
                 // its shift mod 32), unpack row by row through the LUT (all 12 reads ahead of the
