@@ -670,15 +670,17 @@ template <bool YIELD = false>
 __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 {
     if constexpr (YIELD) __builtin_amdgcn_s_setprio(0);
-    int r = -1;
 #pragma clang loop unroll(disable)
     for (int n = 0; n < GOL_SPIN_LIMIT; ++n) {
         const int x = __builtin_amdgcn_readfirstlane(lds_rd32(f));
-        if (x >= v) { r = x; break; }
+        if (x >= v) {
+            if constexpr (YIELD) __builtin_amdgcn_s_setprio(1);
+            return x;
+        }
         __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
     }
     if constexpr (YIELD) __builtin_amdgcn_s_setprio(1);
-    return r;
+    return -1;
 }
 
 // ------------------------------------------------------------------ band layout, split pipeline
