@@ -694,8 +694,11 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 // (work_item).
 // COUNT: the last wave adds the alive cells of the rows it stores to a.slots (branch-free: a
 // per-row uniform mask, no branch around the count as a null-slots check made it).
-template <int KW, int P, bool CONTIG, bool COUNT>
-__global__ void __launch_bounds__(64 * P)
+// NPIPE > 1 (measurement build, GOL_BAND_NPIPE): one workgroup of NPIPE x P waves per CU holds
+// NPIPE pipelines, each on ONE SIMD (pipeline = the SIMD of its waves from HW_ID, stage = the
+// wave's rank there), so a SIMD serves the stages of a single pipeline.
+template <int KW, int P, bool CONTIG, bool COUNT, int NPIPE = 1>
+__global__ void __launch_bounds__(64 * P * NPIPE)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
 band_pipe_kernel(BitsArgs a)
 {
@@ -705,20 +708,39 @@ band_pipe_kernel(BitsArgs a)
     constexpr int U = band_useful_words(K, DW);
     constexpr int ROW = 64 * DW;
     constexpr int NS = 3;
-    __shared__ uint32_t in_ring[NS][3][ROW];
-    __shared__ uint32_t ring[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
-    __shared__ int ready[P], consumed[P];
+    __shared__ uint32_t in_ring_[NPIPE][NS][3][ROW];
+    __shared__ uint32_t ring_[NPIPE][P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
+    __shared__ int ready_[NPIPE][P], consumed_[NPIPE][P];
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (never read; all waves share it)
+    __shared__ int simd_of[NPIPE > 1 ? NPIPE * P : 1];
 
     const int lane = threadIdx.x & 63;
+    int pipe = 0, stage = 0;
+    if constexpr (NPIPE > 1) {
+        const int wave = threadIdx.x >> 6;
+        const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u);
+        if (lane == 0) simd_of[wave] = simd;
+        __syncthreads();
+        int r = 0, cnt[4] = {0, 0, 0, 0};
+        for (int i = 0; i < NPIPE * P; ++i) {
+            const int si = simd_of[i];
+            r += (i < wave) & (si == simd);
+            cnt[si & 3] += 1;
+        }
+        const bool even = NPIPE == 4 && cnt[0] == P && cnt[1] == P && cnt[2] == P && cnt[3] == P;
+        pipe = __builtin_amdgcn_readfirstlane(even ? simd : wave % NPIPE);
+        stage = __builtin_amdgcn_readfirstlane(even ? r : wave / NPIPE);
+    }
+    const int litem = NPIPE > 1 ? (int)blockIdx.x * NPIPE + pipe : (int)blockIdx.x;
     int group, s0, s1, rotv;
-    const bool has_rows = work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, blockIdx.x, group, s0, s1, rotv);
+    const bool has_rows = work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, litem, group, s0, s1, rotv);
     uint32_t *ctr;
-    const int dir = work_dir(a.sm, blockIdx.x, ctr);  // 0: static strip, +1 / -1: paired (StripMap)
+    const int dir = work_dir(a.sm, litem, ctr);  // 0: static strip, +1 / -1: paired (StripMap)
     // Pipeline position of this wave, rotated per workgroup: the waves of a workgroup sit on the
     // CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put its
     // loader (global_load_lds) on one SIMD and its storer on another.
-    const int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
+    const int wv = NPIPE > 1 ? stage : __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
+    uint32_t (*const in_ring)[3][ROW] = in_ring_[pipe];
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
     const int64_t band_q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
@@ -758,13 +780,14 @@ band_pipe_kernel(BitsArgs a)
         }
     };
 
-    if (!has_rows) return;  // whole workgroup (no barrier after this point)
-    if (threadIdx.x < P) { ready[threadIdx.x] = 0; consumed[threadIdx.x] = 0; }
+    if (NPIPE == 1 && !has_rows) return;  // whole workgroup (no barrier after this point)
+    if (threadIdx.x < NPIPE * P) { ready_[threadIdx.x / P][threadIdx.x % P] = 0; consumed_[threadIdx.x / P][threadIdx.x % P] = 0; }
     __syncthreads();
-    lds_u32 *const ring_l = (lds_u32 *)&ring[0][0][0][0];
-    lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0];
-    lds_u32 *const ready_l = (lds_u32 *)&ready[0];
-    lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
+    if (!has_rows) return;  // a pipeline without rows (no barrier after this point)
+    lds_u32 *const ring_l = (lds_u32 *)&ring_[pipe][0][0][0][0];
+    lds_u32 *const in_l = (lds_u32 *)&in_ring_[pipe][0][0][0];
+    lds_u32 *const ready_l = (lds_u32 *)&ready_[pipe][0];
+    lds_u32 *const consumed_l = (lds_u32 *)&consumed_[pipe][0];
     constexpr int SLOT = 3 * ROW;  // uint32 per slot (one block)
 
     Pipe<KW, DW> p;
@@ -2077,10 +2100,27 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 #define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
 static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
 
+#ifndef GOL_BAND_NPIPE
+#define GOL_BAND_NPIPE 1
+#endif
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
     constexpr int KW = 3, P = 4;
+    if constexpr (GOL_BAND_NPIPE > 1) {  // measurement build: pipelines on one SIMD each
+        constexpr int NP = GOL_BAND_NPIPE;
+        const bool count = a.slots != nullptr;
+        const void *kf = (const void *)band_pipe_kernel<KW, P, true, true, NP>;
+        const int64_t slots = resident_workgroups(kf, 64 * P * NP) * NP;
+        if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
+        const int64_t items = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
+        const dim3 g((unsigned)((items + NP - 1) / NP)), b(64 * P * NP);
+        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, NP>), g, b, 0, s, a);
+        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, NP>), g, b, 0, s, a);
+        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, NP>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, NP>), g, b, 0, s, a);
+        return hipGetLastError();
+    }
     const bool count = a.slots != nullptr;
     const void *kf = contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true> : (const void *)band_pipe_kernel<KW, P, true, false>)
                             : (count ? (const void *)band_pipe_kernel<KW, P, false, true> : (const void *)band_pipe_kernel<KW, P, false, false>);
