@@ -339,7 +339,9 @@ static int sync_all(gol_engine *e)
     if (flags) {
         for (auto &s : e->sh) {
             RCCHK(set_dev(s.device));
-            HIPCHK(hipMemset(s.err, 0, sizeof(uint32_t)));
+            HIPCHK(hipMemsetAsync(s.err, 0, sizeof(uint32_t), s.stream));
+            HIPCHK(hipStreamSynchronize(s.stream));
+            HIPCHK(golk_reset_claims(s.device));  // a timed-out pair may have left its claims set
         }
         return gol_set_error(GOL_EHIP, "device fault in a step kernel (error flags 0x%x: %s); the board is not valid",
                              flags, (flags & GOLK_ERR_SPIN) ? "a pipeline wave timed out waiting for its neighbour" : "?");

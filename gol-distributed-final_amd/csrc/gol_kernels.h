@@ -12,6 +12,8 @@
 
 // Per-device error word for launches made without one (lazily allocated, zeroed).
 uint32_t *golk_device_err_word(int device);
+// zero the paired-rank claim counters of every stream on `device` (after a faulted launch)
+hipError_t golk_reset_claims(int device);
 
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k);
 // Standard layout: dw words per lane (1, 2 or 4), k in {1, 2, 4, 8} (and 16 for dw <= 2).

@@ -1842,7 +1842,10 @@ uint32_t *golk_device_err_word(int device)
     int prev = 0;
     uint32_t *w = nullptr;
     if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return nullptr;
-    if (hipMalloc(&w, sizeof(uint32_t)) != hipSuccess || hipMemset(w, 0, sizeof(uint32_t)) != hipSuccess) w = nullptr;
+    // zeroed and synchronised: launches on non-blocking streams are not ordered after the null stream
+    if (hipMalloc(&w, sizeof(uint32_t)) != hipSuccess || hipMemset(w, 0, sizeof(uint32_t)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+        w = nullptr;
     (void)hipSetDevice(prev);
     if (w) words[device] = w;
     return w;
@@ -1982,25 +1985,43 @@ static int device_cus()
 // of the CUs) and every rank still gets >= min_rows rows; else false (equal strips).
 // Claim counters of the paired ranks (StripMap), one zeroed buffer per stream: launches on one
 // stream run in order and leave their counters zeroed; launches on different streams may run
-// at once and must not share counters.
+// at once and must not share counters.  The buffer is zeroed ON that stream (stream-ordered
+// before the launch that asks for it): a null-stream hipMemset is not ordered before work on a
+// non-blocking stream, and a first launch that raced it counted rows twice (overlapping claims;
+// tests/test_gpu_engine.py::test_band_paired_narrow_board).  A launch that faults (a pipeline
+// wave timed out) can leave counters set: golk_reset_claims zeroes a device's buffers again.
+static std::mutex claims_mu;
+static std::map<std::pair<hipStream_t, int>, uint32_t *> claims_bufs;
+static size_t claims_bytes(int cus) { return (size_t)cus * 2 * 16 * sizeof(uint32_t); }
 static uint32_t *claim_counters(hipStream_t s, int cus)
 {
-    static std::mutex mu;
-    static std::map<std::pair<hipStream_t, int>, uint32_t *> bufs;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = bufs.find({s, dev});
-    if (it != bufs.end()) return it->second;
+    std::lock_guard<std::mutex> lock(claims_mu);
+    auto it = claims_bufs.find({s, dev});
+    if (it != claims_bufs.end()) return it->second;
     uint32_t *c = nullptr;
-    const size_t bytes = (size_t)cus * 2 * 16 * sizeof(uint32_t);
-    if (hipMalloc(&c, bytes) != hipSuccess) return nullptr;
-    if (hipMemset(c, 0, bytes) != hipSuccess) {
+    if (hipMalloc(&c, claims_bytes(cus)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(c, 0, claims_bytes(cus), s) != hipSuccess) {
         (void)hipFree(c);
         return nullptr;
     }
-    bufs[{s, dev}] = c;
+    claims_bufs[{s, dev}] = c;
     return c;
+}
+
+hipError_t golk_reset_claims(int device)
+{
+    std::lock_guard<std::mutex> lock(claims_mu);
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    for (auto &kv : claims_bufs) {
+        if (e != hipSuccess) break;
+        if (kv.first.second != device) continue;
+        e = hipMemset(kv.second, 0, claims_bytes(cus));
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();  // the zeroes land before any later launch
+    return e;
 }
 
 static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const double *weight, int64_t min_rows,

@@ -471,6 +471,32 @@ def test_byte_pipe_several_strips(golhip, H, strip):
     assert np.array_equal(got2, O.unpack(O.bits_run(O.pack(board), 32)))
 
 
+def test_byte_pipe_paired_narrow_board(golhip):
+    """Two column groups and enough rows for the one-round rank split with a paired range per
+    CU (two workgroups walking one range from both ends, meeting wherever the faster one got to)
+    plus a lone rank: 32768 x 2112 bytes, two k = 32 launches against the bit oracle."""
+    H, W = 32768, 32 * 66
+    words = O.random_words(5, 0, H, W // 64)
+    board = O.unpack(words)
+    got = _bytes_k_steps(board, 32, 2, 0, [(0, H)])
+    assert O.hash_words(O.pack(got)) == O.hash_words(O.bits_run(words, 64))
+
+
+def test_band_paired_narrow_board(golhip):
+    """One band column group (W = 2048) over 65536 rows: the one-round rank split gives every CU
+    256 rows in two paired ranges of ~128 rows (4K = 48 rows of fill each); 25 turns (two k = 12
+    launches and a 1-turn one) against the bit oracle."""
+    H, W = 65536, 2048
+    with golhip.Engine(H, W, device=0) as e:
+        assert e.info()["layout"] == "band" and e.info()["turns_per_launch"] == 12
+        e.load_random(11)
+        counts = e.step_counted(24, 12)
+        e.step(1)
+        ref, rc = O.bits_run(O.random_words(11, 0, H, W // 64), 25, with_counts=True)
+        assert counts.tolist() == [rc[11], rc[23]]
+        assert e.hash() == O.hash_words(ref)
+
+
 def test_byte16k_full_size_parity(golhip):
     """Config 2 at its size: the 16384 x 16384 byte board, two k = 32 launches (the bench's
     kernel, automatic strips: many strips per column group) against the bit oracle's 64 turns."""
