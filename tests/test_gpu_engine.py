@@ -482,6 +482,23 @@ def test_byte_pipe_paired_narrow_board(golhip):
     assert O.hash_words(O.pack(got)) == O.hash_words(O.bits_run(words, 64))
 
 
+def test_byte_board_engine_counted_paired(golhip):
+    """A width that is a multiple of 32 but not of 64 keeps the engine on the 0/255 byte board:
+    with k = 32 its launches take the byte pipeline's one-round rank split (paired ranges); the
+    alive count of every launch (fused) and the board against the literal port (16 threads)."""
+    H, W = 28672, 32 * 65
+    rng = np.random.default_rng(2080)
+    board = (rng.random((H, W)) < 0.35).astype(np.uint8) * 255
+    with golhip.Engine(H, W, device=0, turns_per_launch=32) as e:
+        e.load_bytes(board)
+        counts = e.step_counted(64, 32)
+        got = e.store_bytes()
+    mid = O.run(board, 32, 16)
+    ref = O.run(mid, 32, 16)
+    assert counts.tolist() == [int(np.count_nonzero(mid)), int(np.count_nonzero(ref))]
+    assert np.array_equal(got, ref)
+
+
 def test_band_paired_narrow_board(golhip):
     """One band column group (W = 2048) over 65536 rows: the one-round rank split gives every CU
     256 rows in two paired ranges of ~128 rows (4K = 48 rows of fill each); 25 turns (two k = 12
