@@ -78,6 +78,33 @@ def test_tiny_shards_cap_turns_per_launch(G, H, n, W, layout):
         assert e.hash() == O.hash_words(ref)
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_concurrent_shards_paired_ranges(G, n):
+    """Shards on one GPU launch on their own streams at once; each launch of a narrow band board
+    takes the one-round rank split with paired ranges and its own claim counters.  Counted steps
+    (the first launch of every fresh stream included) and the board against the oracle."""
+    H, W = 65536 * n, 2048
+    words = O.random_words(21 + n, 0, H, W // 64)
+    ref, counts = O.bits_run(words, 36, with_counts=True)
+    with _sharded(G, H, W, n) as e:
+        e.load_random(21 + n)
+        assert e.step_counted(36, 12).tolist() == [counts[11], counts[23], counts[35]]
+        assert e.hash() == O.hash_words(ref)
+
+
+def test_engines_in_sequence_reuse_streams(G):
+    """Engines created and destroyed one after another (a new engine may get a destroyed one's
+    stream handle, and with it that stream's claim counters): the first counted launch of each is
+    exact, for band boards of 1, 2, 1 and 4 column groups."""
+    for H, W, seed in ((65536, 2048, 1), (32768, 4096, 2), (65536, 1024, 3), (16384, 8192, 4)):
+        words = O.random_words(seed, 0, H, W // 64)
+        ref, counts = O.bits_run(words, 12, with_counts=True)
+        with G.Engine(H, W, device=0) as e:
+            e.load_random(seed)
+            assert e.step_counted(12, 12).tolist() == [counts[11]], (H, W)
+            assert e.hash() == O.hash_words(ref), (H, W)
+
+
 @pytest.mark.parametrize("H,W", [(16, 16), (33, 32), (20, 48), (9, 8)])
 def test_narrow_boards_byte_path(G, H, W):
     """Widths below 64 (or not a multiple of 64) run on the exact byte board: vs the literal port."""
