@@ -23,7 +23,7 @@ LIB = os.environ.get("GOL_TL_LIB") or os.path.join(ROOT, "tools", "tl", "libtime
 ENTRY = "    const int lane = threadIdx.x & 63;\n"
 STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n    const uint64_t tl_c0 = __builtin_amdgcn_s_memtime(); (void)tl_c0;\n"
 EXIT_BAND = "    if (COUNT && wv == P - 1) slot_add(a.slots, alive);\n}"
-EXIT_BYTES = "    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);\n    if (a.slots && wv == P - 1) slot_add(a.slots, alive);\n}"
+EXIT_BYTES = "    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);\n    if (COUNT && wv == P - 1) slot_add(a.slots, alive);\n}"
 STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear workgroup id * P + wave
         const uint64_t tl_t1 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
