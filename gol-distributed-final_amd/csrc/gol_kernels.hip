@@ -2098,7 +2098,7 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
 #define GOL_BAND_RANK_W 0.25, 0.25, 0.25, 0.25
 #endif
 #ifndef GOL_BYTES_RANK_W
-#define GOL_BYTES_RANK_W 0.4457, 0.3094, 0.2449, 0.0
+#define GOL_BYTES_RANK_W 0.4457, 0.33, 0.2449, 0.0  // lone rank 1: 0.31 -> 0.33 after the fill skip (+1.3 %)
 #endif
 static const double BAND_PIPE_RANK_W[4] = {GOL_BAND_RANK_W};
 static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
