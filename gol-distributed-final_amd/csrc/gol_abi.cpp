@@ -215,7 +215,7 @@ extern "C" int gol_dev_error(int32_t device, uint32_t *flags)
     uint32_t v = 0;
     hipError_t he = hipMemcpy(&v, w, sizeof v, hipMemcpyDeviceToHost);
     if (he == hipSuccess && v) he = hipMemset(w, 0, sizeof v);
-    if (he == hipSuccess && v) he = golk_reset_claims(dev);  // a timed-out pair may have left its claims set
+    if (he == hipSuccess && v) he = golk_reset_claims_device(dev);  // a timed-out pair may have left its claims set
     (void)hipSetDevice(prev);
     if (he != hipSuccess) return gol_set_error(GOL_EHIP, "error word: %s", hipGetErrorString(he));
     *flags = v;

@@ -13,6 +13,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -100,8 +102,11 @@ static void shard_release(gol_shard &s)
 {
     (void)hipSetDevice(s.device);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.edge) (void)hipStreamSynchronize(s.edge);
     if (s.comm) (void)hipStreamSynchronize(s.comm);
     if (s.nccl) (void)ncclCommDestroy(s.nccl);
+    if (s.stream) golk_release_claims(s.stream);
+    if (s.edge) golk_release_claims(s.edge);
     for (auto &b : s.bits_alloc)
         if (b) (void)hipFree(b);
     free_exact_bytes(s);
@@ -113,20 +118,20 @@ static void shard_release(gol_shard &s)
     if (s.staging) (void)hipFree(s.staging);
     if (s.host_staging) (void)hipHostFree(s.host_staging);
     for (auto ev : s.tev) (void)hipEventDestroy(ev);
-    if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
-    if (s.ev_comm) (void)hipEventDestroy(s.ev_comm);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
-    if (s.comm) (void)hipStreamDestroy(s.comm);
+    for (hipEvent_t ev : {s.ev_start, s.ev_edge, s.ev_halo})
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t st : {s.stream, s.edge, s.comm})
+        if (st) (void)hipStreamDestroy(st);
     s = gol_shard();
 }
 
 static int shard_alloc(gol_engine *e, gol_shard &s)
 {
     RCCHK(set_dev(s.device));
-    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.ev_comm, hipEventDisableTiming));
+    for (hipStream_t *st : {&s.stream, &s.edge, &s.comm}) HIPCHK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+    golk_own_stream(s.stream);
+    golk_own_stream(s.edge);
+    for (hipEvent_t *ev : {&s.ev_start, &s.ev_edge, &s.ev_halo}) HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     HIPCHK(hipMalloc(&s.slots, SLOT_BYTES));
     HIPCHK(hipMalloc(&s.flag, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&s.err, sizeof(uint32_t)));
@@ -175,6 +180,7 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
     if (layout == GOL_LAYOUT_BAND && W % 1024 != 0) return gol_set_error(GOL_EINVAL, "the band layout needs W %% 1024 == 0");
     e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
     if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
+    e->step_flags = cfg ? (cfg->flags & GOL_STEP_SERIAL) : 0;
     return GOL_OK;
 }
 
@@ -186,6 +192,8 @@ static int engine_shards(gol_engine *e, const std::vector<int> &devices)
     if (e->H < e->nranks)
         return gol_set_error(GOL_EINVAL, "%d shards cannot split %lld rows", e->nranks, (long long)e->H);
     e->min_rows = e->H / e->nranks;  // broker.go:172-206: the smallest shard
+    // every exchange carries the rows of the longest launch the engine makes
+    e->kx = pick_k(e->k, INT64_MAX, e->min_rows, e->band_capable ? e->band_dw : e->dw, e->band_capable);
     e->sh.resize(devices.size());
     for (size_t i = 0; i < devices.size(); ++i) {
         gol_shard &s = e->sh[i];
@@ -323,26 +331,37 @@ extern "C" int gol_engine_shard(gol_engine *e, int32_t i, int32_t *device, int64
 // ------------------------------------------------------------------ synchronisation, errors
 // Wait for every shard's work and read the shards' device error words (one pinned readback
 // queued behind the work, so the check costs no extra synchronisation).
+// With ranks in several processes the error words are all-reduced first (ncclMax), so a fault
+// on one rank -- whose rows reach the others through the halo -- fails the call on every rank.
 static int sync_all(gol_engine *e)
 {
+    const bool several = e->rank_mode && e->nranks > 1;
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));  // (the edge launches' error word writes)
+        if (several) NCCLCHK(ncclAllReduce(s.err, s.err, 1, ncclUint32, ncclMax, s.nccl, s.stream));
         HIPCHK(hipMemcpyAsync(s.host_word, s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
     }
     uint32_t flags = 0;
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipStreamSynchronize(s.edge));
         HIPCHK(hipStreamSynchronize(s.comm));
         flags |= s.host_word[0];
     }
+    e->halo_issued = false;
     if (flags) {
         for (auto &s : e->sh) {
             RCCHK(set_dev(s.device));
             HIPCHK(hipMemsetAsync(s.err, 0, sizeof(uint32_t), s.stream));
+            // a timed-out pair may have left its claims set: this engine's streams only
+            HIPCHK(golk_reset_claims(s.stream));
+            HIPCHK(golk_reset_claims(s.edge));
             HIPCHK(hipStreamSynchronize(s.stream));
-            HIPCHK(golk_reset_claims(s.device));  // a timed-out pair may have left its claims set
+            HIPCHK(hipStreamSynchronize(s.edge));
         }
+        e->halo_ok = false;
         return gol_set_error(GOL_EHIP, "device fault in a step kernel (error flags 0x%x: %s); the board is not valid",
                              flags, (flags & GOLK_ERR_SPIN) ? "a pipeline wave timed out waiting for its neighbour" : "?");
     }
@@ -362,12 +381,28 @@ static int rank_barrier(gol_engine *e)
     return GOL_OK;
 }
 
+// The board is about to change outside a step (load, layout conversion, exact first turn):
+// the halo of the current buffer is no longer the board's, and the exchange still in flight
+// (it reads and writes the buffers) finishes before the compute stream writes them.
+static int invalidate_halo(gol_engine *e)
+{
+    if (e->halo_issued)
+        for (auto &s : e->sh) {
+            RCCHK(set_dev(s.device));
+            HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
+            for (auto &t : e->sh) HIPCHK(hipStreamWaitEvent(s.stream, t.ev_halo, 0));  // (loopback: t reads my rows)
+        }
+    e->halo_ok = false;
+    return GOL_OK;
+}
+
 // ------------------------------------------------------------------ layout conversion
 // The band layout is a stepping detail: convert on the first step, convert back before
 // anything reads the bits.  Both are one HBM pass (32x32 bit transposes) per shard.
 static int convert(gol_engine *e, bool to_band)
 {
     if (e->band == to_band || e->mode != GOL_MODE_BITS) return GOL_OK;
+    RCCHK(invalidate_halo(e));
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         HIPCHK(golk_band_convert(to_band, s.bits[e->cur], s.bits[1 - e->cur], s.R, e->Wd, e->pitch, e->pitch, s.stream));
@@ -378,7 +413,7 @@ static int convert(gol_engine *e, bool to_band)
 }
 static int ensure_standard(gol_engine *e) { return convert(e, false); }
 
-// ------------------------------------------------------------------ one k-turn launch
+// ------------------------------------------------------------------ one k-turn step
 static int copy_rows(gol_shard &dst_s, uint32_t *dst, const gol_shard &src_s, const uint32_t *src, size_t bytes,
                      hipStream_t st)
 {
@@ -387,134 +422,202 @@ static int copy_rows(gol_shard &dst_s, uint32_t *dst, const gol_shard &src_s, co
     return GOL_OK;
 }
 
-// Halo rows of the current input buffer: shard r's ghost rows [-k, 0) <- the last k rows of
-// shard r-1, ghost rows [R, R+k) <- the first k rows of shard r+1 (mod nranks).
-static int exchange(gol_engine *e, int k)
+// The halo plan of local shard i (gol_halo_plan: the schedule golhip.sharded runs as well).
+static int plan_of(gol_engine *e, int i, gol_halo_op (&ops)[4])
+{
+    int32_t n = 0;
+    RCCHK(gol_halo_plan(e->H, e->nranks, e->rank + i, e->kx, ops, 4, &n));
+    return n == 4 ? GOL_OK : gol_set_error(GOL_EINVAL, "halo plan of %d ops", n);
+}
+
+// Exchange the kx halo rows of bits[cur] on the comm streams, once every shard's ev_edge (the
+// rows it sends are written) has been recorded; records ev_halo.  Every transport runs the
+// shards' gol_halo_plan in issue order.  LOCAL / LOOPBACK execute it as device copies, pairing
+// each receive with the sender's matching send exactly as RCCL does (the n-th receive of shard
+// s from shard p gets p's n-th send to s), so the one-GPU loopback tests exercise the RCCL
+// matching of the same plan, including nranks = 2 (one peer on both sides) and the one-shard
+// torus wrap (a shard sending to itself).
+static int exchange(gol_engine *e)
 {
     const int n = (int)e->sh.size();
     const int c = e->cur;
     const int64_t P = e->pitch;
-    const size_t hb = (size_t)k * P * sizeof(uint32_t);
-    if (e->transport == GOL_TRANSPORT_LOCAL) {  // one shard = the whole torus: wrap rows on its own stream
-        gol_shard &s = e->sh[0];
-        uint32_t *mid = s.bits[c];
-        RCCHK(set_dev(s.device));
-        HIPCHK(hipMemcpyAsync(mid - k * P, mid + (s.R - k) * P, hb, hipMemcpyDeviceToDevice, s.stream));
-        HIPCHK(hipMemcpyAsync(mid + s.R * P, mid, hb, hipMemcpyDeviceToDevice, s.stream));
-        return GOL_OK;
+    const size_t hb = (size_t)e->kx * P * sizeof(uint32_t);
+    std::vector<std::array<gol_halo_op, 4>> plans(n);
+    for (int i = 0; i < n; ++i) {
+        gol_halo_op ops[4];
+        RCCHK(plan_of(e, i, ops));
+        std::copy(ops, ops + 4, plans[i].begin());
     }
-    for (auto &s : e->sh) {
-        RCCHK(set_dev(s.device));
-        HIPCHK(hipEventRecord(s.ev_ready, s.stream));
-    }
-    if (e->transport == GOL_TRANSPORT_LOOPBACK) {
+    auto local = [&](int global) { return global - e->rank; };  // local shard index of a global rank
+    if (e->transport != GOL_TRANSPORT_RCCL) {
         for (int i = 0; i < n; ++i) {
-            gol_shard &s = e->sh[i], &p = e->sh[(i + n - 1) % n], &q = e->sh[(i + 1) % n];
+            gol_shard &s = e->sh[i];
             RCCHK(set_dev(s.device));
-            HIPCHK(hipStreamWaitEvent(s.comm, s.ev_ready, 0));  // my ghost rows are no longer read
-            HIPCHK(hipStreamWaitEvent(s.comm, p.ev_ready, 0));  // the neighbours' rows are written
-            HIPCHK(hipStreamWaitEvent(s.comm, q.ev_ready, 0));
-            RCCHK(copy_rows(s, s.bits[c] - k * P, p, p.bits[c] + (p.R - k) * P, hb, s.comm));
-            RCCHK(copy_rows(s, s.bits[c] + s.R * P, q, q.bits[c], hb, s.comm));
-            HIPCHK(hipEventRecord(s.ev_comm, s.comm));
+            // my ghost rows are no longer read (my edge launches) and the rows my peers send me
+            // are written (theirs)
+            for (const auto &op : plans[i])
+                HIPCHK(hipStreamWaitEvent(s.comm, e->sh[local(op.peer)].ev_edge, 0));
+            for (int j = 0; j < 4; ++j) {
+                const gol_halo_op &rv = plans[i][j];
+                if (rv.kind != GOL_HALO_RECV) continue;
+                int nth = 0;  // this is my nth receive from rv.peer
+                for (int jj = 0; jj < j; ++jj) nth += plans[i][jj].kind == GOL_HALO_RECV && plans[i][jj].peer == rv.peer;
+                const int p = local(rv.peer);
+                const gol_halo_op *sd = nullptr;  // the peer's nth send to me
+                for (int m = 0, cnt = 0; m < 4 && !sd; ++m) {
+                    const gol_halo_op &o = plans[p][m];
+                    if (o.kind == GOL_HALO_SEND && o.peer == e->rank + i && cnt++ == nth) sd = &o;
+                }
+                if (!sd || sd->rows != rv.rows) return gol_set_error(GOL_EINVAL, "halo plan: unmatched receive");
+                gol_shard &ps = e->sh[p];
+                RCCHK(copy_rows(s, s.bits[c] + rv.row * P, ps, ps.bits[c] + sd->row * P, hb, s.comm));
+            }
+            HIPCHK(hipEventRecord(s.ev_halo, s.comm));
         }
+        e->halo_issued = true;
         return GOL_OK;
     }
     // RCCL: one group over every local shard (ncclCommInitAll comms must be driven together).
-    // For two ranks both neighbours are the same peer: the issue order pairs my first send
-    // (top rows) with the peer's first receive (its bottom ghost rows), as the ring requires.
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
-        HIPCHK(hipStreamWaitEvent(s.comm, s.ev_ready, 0));
+        HIPCHK(hipStreamWaitEvent(s.comm, s.ev_edge, 0));
     }
-    const size_t cnt = (size_t)k * P;
     ncclResult_t first = ncclGroupStart();
     for (int i = 0; i < n && first == ncclSuccess; ++i) {
         gol_shard &s = e->sh[i];
-        const int N = e->nranks, r = e->rank + i;
-        const int prev = (r + N - 1) % N, next = (r + 1) % N;
         uint32_t *mid = s.bits[c];
-        ncclResult_t x;
-        if ((x = ncclSend(mid, cnt, ncclUint32, prev, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
-        if ((x = ncclRecv(mid + s.R * P, cnt, ncclUint32, next, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
-        if ((x = ncclSend(mid + (s.R - k) * P, cnt, ncclUint32, next, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
-        if ((x = ncclRecv(mid - k * P, cnt, ncclUint32, prev, s.nccl, s.comm)) != ncclSuccess && first == ncclSuccess) first = x;
+        for (const auto &op : plans[i]) {
+            const size_t cnt = (size_t)op.rows * P;
+            const ncclResult_t x = op.kind == GOL_HALO_SEND
+                                       ? ncclSend(mid + op.row * P, cnt, ncclUint32, op.peer, s.nccl, s.comm)
+                                       : ncclRecv(mid + op.row * P, cnt, ncclUint32, op.peer, s.nccl, s.comm);
+            if (x != ncclSuccess && first == ncclSuccess) first = x;
+        }
     }
     const ncclResult_t end = ncclGroupEnd();
     if (first != ncclSuccess || end != ncclSuccess)
         return gol_set_error(GOL_ECOMM, "halo exchange: %s", ncclGetErrorString(first != ncclSuccess ? first : end));
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
-        HIPCHK(hipEventRecord(s.ev_comm, s.comm));
+        HIPCHK(hipEventRecord(s.ev_halo, s.comm));
     }
+    e->halo_issued = true;
     return GOL_OK;
 }
 
-static int shard_kernel(gol_engine *e, int i, int k, int64_t row0, int64_t rows, uint64_t *slots, bool timed)
+// Exchange the halo of the board as it stands (after a load, a conversion or a step outside
+// launch_k): the sent rows are whatever the compute stream wrote last.
+static int exchange_current(gol_engine *e)
 {
-    gol_shard &s = e->sh[i];
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
+        HIPCHK(hipEventRecord(s.ev_edge, s.stream));
+    }
+    RCCHK(exchange(e));
+    e->halo_ok = true;
+    return GOL_OK;
+}
+
+static int step_launch(gol_engine *e, gol_shard &s, hipStream_t st, int k, int64_t row0, int64_t rows, uint64_t *slots)
+{
     if (rows <= 0) return GOL_OK;
     uint32_t *mid = s.bits[e->cur];
     const uint32_t *top = mid - (int64_t)k * e->pitch, *bot = mid + s.R * e->pitch;
     uint32_t *dst = s.bits[1 - e->cur];
-    timed = timed && e->timing;
-    size_t ev = 0;
-    if (timed) {
-        if (s.tused + 2 > s.tev.size()) {
-            for (int j = 0; j < 2; ++j) {
-                hipEvent_t x;
-                HIPCHK(hipEventCreate(&x));
-                s.tev.push_back(x);
-            }
-        }
-        ev = s.tused;
-        s.tused += 2;
-        HIPCHK(hipEventRecord(s.tev[ev], s.stream));
-    }
     if (e->band)
-        HIPCHK(golk_band_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->band_dw, e->strip, slots, s.err,
-                              s.stream));
+        HIPCHK(golk_band_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->band_dw, e->strip, slots, s.err, st));
     else
-        HIPCHK(golk_bits_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->dw, e->strip, slots, s.stream));
-    if (timed) {
-        HIPCHK(hipEventRecord(s.tev[ev + 1], s.stream));
-        e->timed.push_back({i, ev, (double)rows * (double)e->W * k});
-    }
+        HIPCHK(golk_bits_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->dw, e->strip, slots, st));
     return GOL_OK;
 }
 
-// k turns of every shard: halo exchange, the interior rows [k, R-k) (they need no halo, so
-// they overlap the exchange), then the boundary rows once the halo is in.  With `count` the
-// alive cells of the output are added to each shard's slots.
+// Timing of one shard-step: events on the compute stream from the step's start to its end
+// (the edge stream joined).  The pool is folded into running sums when it is full.
+static int fold_timing(gol_engine *e)
+{
+    for (const auto &t : e->timed) {
+        gol_shard &s = e->sh[t.shard];
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipEventSynchronize(s.tev[t.ev + 1]));
+        float x = 0;
+        HIPCHK(hipEventElapsedTime(&x, s.tev[t.ev], s.tev[t.ev + 1]));
+        e->t_ms += x;
+        e->t_cells += t.cell_updates;
+        e->t_n += 1;
+    }
+    e->timed.clear();
+    for (auto &s : e->sh) s.tused = 0;
+    return GOL_OK;
+}
+
+static int timing_event(gol_engine *e, gol_shard &s, size_t *ev)
+{
+    if (s.tused + 2 > GOL_TIMING_EVENTS) RCCHK(fold_timing(e));
+    while (s.tused + 2 > s.tev.size()) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreate(&x));
+        s.tev.push_back(x);
+    }
+    *ev = s.tused;
+    s.tused += 2;
+    return GOL_OK;
+}
+
+// k turns of every shard, as gol_step_plan lays them out: the edge rows (they read the halo)
+// on the edge stream and the interior beside them on the compute stream; the next step's halo
+// exchange starts as soon as the edge rows are written, while the interior is still running.
+// With `count` the alive cells of the output are added to each shard's slots.
 static int launch_k(gol_engine *e, int k, bool count)
 {
-    RCCHK(exchange(e, k));
+    if (k > e->kx) return gol_set_error(GOL_EINVAL, "k %d > the exchanged halo (%d rows)", k, e->kx);
+    if (!e->halo_ok) RCCHK(exchange_current(e));
     const int n = (int)e->sh.size();
     for (int i = 0; i < n; ++i) {
         gol_shard &s = e->sh[i];
         RCCHK(set_dev(s.device));
+        gol_launch plan[3];
+        int32_t np = 0;
+        RCCHK(gol_step_plan(s.R, k, e->kx, e->step_flags, plan, 3, &np));
         uint64_t *slots = count ? s.slots : nullptr;
         if (count) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
-        if (e->transport == GOL_TRANSPORT_LOCAL) {
-            RCCHK(shard_kernel(e, i, k, 0, s.R, slots, true));
-            continue;
+        size_t ev = 0;
+        if (e->timing) {
+            RCCHK(timing_event(e, s, &ev));
+            HIPCHK(hipEventRecord(s.tev[ev], s.stream));
         }
-        const bool interior = s.R >= 3 * k;
-        if (interior) RCCHK(shard_kernel(e, i, k, k, s.R - 2 * k, slots, true));
-        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_comm, 0));
-        if (e->transport == GOL_TRANSPORT_LOOPBACK && n > 1) {
-            // the neighbours copy from my rows: my next launch (which overwrites them) waits
-            HIPCHK(hipStreamWaitEvent(s.stream, e->sh[(i + n - 1) % n].ev_comm, 0));
-            HIPCHK(hipStreamWaitEvent(s.stream, e->sh[(i + 1) % n].ev_comm, 0));
+        HIPCHK(hipEventRecord(s.ev_start, s.stream));  // the step's inputs are complete, slots zeroed
+        bool edge_used = false, waited[2] = {false, false};
+        for (int j = 0; j < np; ++j) {
+            const gol_launch &L = plan[j];
+            const bool on_edge = L.stream == GOL_LAUNCH_EDGE;
+            hipStream_t st = on_edge ? s.edge : s.stream;
+            if (on_edge && !edge_used) HIPCHK(hipStreamWaitEvent(st, s.ev_start, 0));
+            edge_used |= on_edge;
+            if (L.needs_halo && !waited[on_edge]) {
+                waited[on_edge] = true;
+                // the halo is in; and my rows the peers' copies read (LOCAL / LOOPBACK) are no
+                // longer read when this launch overwrites them
+                for (auto &t : e->sh) HIPCHK(hipStreamWaitEvent(st, t.ev_halo, 0));
+            }
+            RCCHK(step_launch(e, s, st, k, L.row0, L.rows, slots));
         }
-        if (interior) {
-            RCCHK(shard_kernel(e, i, k, 0, k, slots, false));
-            RCCHK(shard_kernel(e, i, k, s.R - k, k, slots, false));
+        if (edge_used) {
+            HIPCHK(hipEventRecord(s.ev_edge, s.edge));
+            HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
         } else {
-            RCCHK(shard_kernel(e, i, k, 0, s.R, slots, true));
+            HIPCHK(hipEventRecord(s.ev_edge, s.stream));
+        }
+        if (e->timing) {
+            HIPCHK(hipEventRecord(s.tev[ev + 1], s.stream));
+            e->timed.push_back({i, ev, (double)s.R * (double)e->W * k});
         }
     }
     e->cur = 1 - e->cur;
+    // the next step's halo: waits only for each shard's ev_edge
+    RCCHK(exchange(e));
+    e->halo_ok = true;
     return GOL_OK;
 }
 
@@ -522,6 +625,7 @@ static int launch_k(gol_engine *e, int k, bool count)
 // exact byte kernel over its R rows plus the two halo rows it loaded, then packs the result.
 static int exact_turn(gol_engine *e)
 {
+    RCCHK(invalidate_halo(e));
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         HIPCHK(golk_bytes_step(s.bytes[0], s.R + 2, e->W, e->bstride, 1, s.R + 1, s.bytes[1], e->bstride, s.stream));
@@ -739,18 +843,20 @@ static int alloc_exact_bytes(gol_engine *e, gol_shard &s)
     return GOL_OK;
 }
 
-static void reset_board_state(gol_engine *e)
+static int reset_board_state(gol_engine *e)
 {
+    RCCHK(invalidate_halo(e));
     e->turn = 0;
     e->band = false;
     e->cur = 0;
     e->bcur = 0;
+    return GOL_OK;
 }
 
 extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_t stride)
 {
     if (!e || !world || stride < e->W) return gol_set_error(GOL_EINVAL, "bad load arguments");
-    reset_board_state(e);
+    RCCHK(reset_board_state(e));
     if (e->mode == GOL_MODE_BYTES || !e->bit_capable) {  // one shard, byte board
         gol_shard &s = e->sh[0];
         RCCHK(set_dev(s.device));
@@ -800,7 +906,7 @@ extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
 {
     if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
     if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "random boards need W %% 64 == 0");
-    reset_board_state(e);
+    RCCHK(reset_board_state(e));
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         free_exact_bytes(s);
@@ -876,7 +982,7 @@ struct FileRows {
 
 static int load_pgm_impl(gol_engine *e, const FileRows &fr)
 {
-    reset_board_state(e);
+    RCCHK(reset_board_state(e));
     if (e->mode == GOL_MODE_BYTES || !e->bit_capable) {  // one shard, small byte board
         std::vector<uint8_t> all(e->H * e->W);
         RCCHK(pread_all(fr.fd, all.data(), all.size(), fr.data));
@@ -1106,20 +1212,104 @@ extern "C" int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, in
     return GOL_OK;
 }
 
-extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
+// writePgmImage's byte stream (gol/io.go:52-81): the header (rank 0) and this process's rows at
+// their file offsets, chunk by chunk (device unpack -> pinned staging), into `sink`.
+static int pgm_stream(gol_engine *e, gol_write_fn sink, void *user, int64_t *hlen_out)
 {
-    if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
     RCCHK(ensure_standard(e));
     char header[96];
     const int hlen = snprintf(header, sizeof header, "P5\n%lld %lld\n255\n", (long long)e->W, (long long)e->H);  // io.go:52-59
+    *hlen_out = hlen;
+    const bool several = e->rank_mode && e->nranks > 1;
+    if (!several || e->rank == 0) {
+        if (sink(user, 0, (const uint8_t *)header, hlen) != 0) return gol_set_error(GOL_EIO, "the PGM sink failed (header)");
+    }
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        RCCHK(ensure_staging(e, s));
+        const int64_t r0 = e->mode == GOL_MODE_BYTES ? 0 : s.y0, r1 = e->mode == GOL_MODE_BYTES ? e->H : s.y1;
+        if (e->mode != GOL_MODE_BITS || s.stage_rows < 2) {
+            for (int64_t y = r0; y < r1; y += s.stage_rows) {
+                const int64_t n = std::min(s.stage_rows, r1 - y);
+                RCCHK(shard_rows_to_host(e, s, y, y + n, s.host_staging, e->W));
+                if (sink(user, hlen + y * e->W, s.host_staging, n * e->W) != 0)
+                    return gol_set_error(GOL_EIO, "the PGM sink failed at row %lld", (long long)y);
+            }
+            continue;
+        }
+        // bit board: two halves of the staging buffers; chunk i+1 is unpacked and copied to the
+        // host while the sink consumes chunk i
+        const int64_t half = s.stage_rows / 2;
+        hipEvent_t done[2] = {nullptr, nullptr};
+        int rc = GOL_OK;
+        for (auto &d : done)
+            if (rc == GOL_OK && hipEventCreateWithFlags(&d, hipEventDisableTiming) != hipSuccess)
+                rc = gol_set_error(GOL_EHIP, "event for the PGM stream");
+        auto enqueue = [&](int64_t y, int h) -> int {
+            const int64_t n = std::min(half, r1 - y);
+            uint8_t *dst = s.staging + h * half * e->bstride;
+            HIPCHK(golk_unpack(s.bits[e->cur] + (y - s.y0) * e->pitch, n, e->W, e->pitch, dst, e->bstride, s.stream));
+            HIPCHK(hipMemcpy2DAsync(s.host_staging + h * half * e->W, e->W, dst, e->bstride, e->W, n, hipMemcpyDeviceToHost,
+                                    s.stream));
+            HIPCHK(hipEventRecord(done[h], s.stream));
+            return GOL_OK;
+        };
+        if (rc == GOL_OK) rc = enqueue(r0, 0);
+        for (int64_t y = r0, i = 0; y < r1 && rc == GOL_OK; y += half, ++i) {
+            const int h = (int)(i & 1);
+            if (y + half < r1) rc = enqueue(y + half, 1 - h);  // the other half's sink call has returned
+            if (rc == GOL_OK && hipEventSynchronize(done[h]) != hipSuccess) rc = gol_set_error(GOL_EHIP, "PGM stream copy");
+            if (rc == GOL_OK && sink(user, hlen + y * e->W, s.host_staging + h * half * e->W, std::min(half, r1 - y) * e->W) != 0)
+                rc = gol_set_error(GOL_EIO, "the PGM sink failed at row %lld", (long long)y);
+        }
+        (void)hipStreamSynchronize(s.stream);
+        for (auto d : done)
+            if (d) (void)hipEventDestroy(d);
+        RCCHK(rc);
+    }
+    return GOL_OK;
+}
+
+struct FdSink {
+    int fd;
+};
+static int fd_sink(void *user, int64_t off, const uint8_t *data, int64_t len)
+{
+    const int fd = static_cast<FdSink *>(user)->fd;
+    while (len > 0) {
+        const ssize_t w = pwrite(fd, data, (size_t)len, off);
+        if (w <= 0) return -1;
+        data += w;
+        len -= w;
+        off += w;
+    }
+    return 0;
+}
+
+extern "C" int gol_engine_write_pgm_to(gol_engine *e, gol_write_fn sink, void *user)
+{
+    if (!e || !sink) return gol_set_error(GOL_EINVAL, "bad arguments");
+    int64_t hlen = 0;
+    int rc = pgm_stream(e, sink, user, &hlen);
+    if (e->rank_mode && e->nranks > 1) {
+        const int rb = rank_barrier(e);  // every rank's rows are in its sink when any rank returns
+        if (rc == GOL_OK) rc = rb;
+    }
+    return rc;
+}
+
+extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
+{
+    if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
     const bool several = e->rank_mode && e->nranks > 1;
     int rc = GOL_OK;
     if (!several || e->rank == 0) {
+        char header[96];
+        const int hlen = snprintf(header, sizeof header, "P5\n%lld %lld\n255\n", (long long)e->W, (long long)e->H);
         const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
         if (fd < 0) rc = gol_set_error(GOL_EIO, "cannot create %s", path);
         else {
-            if (write(fd, header, hlen) != hlen) rc = gol_set_error(GOL_EIO, "short write to %s", path);
-            else if (several && ftruncate(fd, hlen + e->H * e->W) != 0) rc = gol_set_error(GOL_EIO, "cannot size %s", path);
+            if (ftruncate(fd, hlen + e->H * e->W) != 0) rc = gol_set_error(GOL_EIO, "cannot size %s", path);
             if (close(fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
         }
     }
@@ -1127,27 +1317,68 @@ extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
         const int rb = rank_barrier(e);  // the file exists and is sized before any rank writes
         if (rc == GOL_OK) rc = rb;
     }
-    const int fd = rc == GOL_OK ? open(path, O_WRONLY) : -1;
-    if (rc == GOL_OK && fd < 0) rc = gol_set_error(GOL_EIO, "cannot open %s", path);
-    for (auto &s : e->sh) {
-        if (rc != GOL_OK) break;
-        rc = set_dev(s.device);
-        if (rc == GOL_OK) rc = ensure_staging(e, s);
-        const int64_t r0 = e->mode == GOL_MODE_BYTES ? 0 : s.y0, r1 = e->mode == GOL_MODE_BYTES ? e->H : s.y1;
-        for (int64_t y = r0; y < r1 && rc == GOL_OK; y += s.stage_rows) {
-            const int64_t n = std::min(s.stage_rows, r1 - y);
-            rc = shard_rows_to_host(e, s, y, y + n, s.host_staging, e->W);
-            const size_t bytes = (size_t)(n * e->W);
-            if (rc == GOL_OK && pwrite(fd, s.host_staging, bytes, hlen + y * e->W) != (ssize_t)bytes)
-                rc = gol_set_error(GOL_EIO, "short write to %s", path);
-        }
+    FdSink fs{rc == GOL_OK ? open(path, O_WRONLY) : -1};
+    if (rc == GOL_OK && fs.fd < 0) rc = gol_set_error(GOL_EIO, "cannot open %s", path);
+    int64_t hlen = 0;
+    if (rc == GOL_OK) {
+        rc = pgm_stream(e, fd_sink, &fs, &hlen);
+        if (rc == GOL_EIO) gol_set_error(GOL_EIO, "short write to %s", path);
     }
-    if (fd >= 0 && close(fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
+    if (fs.fd >= 0 && close(fs.fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
     if (several) {
         const int rb = rank_barrier(e);  // every rank's rows are written when any rank returns
         if (rc == GOL_OK) rc = rb;
     }
     return rc;
+}
+
+// ------------------------------------------------------------------ bit-packed rows in / out
+static int rows_check(gol_engine *e, int64_t y0, int64_t y1, const void *p, int64_t stride)
+{
+    if (!e || !p || y0 < 0 || y1 > e->H || y0 > y1 || stride < e->W / 64)
+        return gol_set_error(GOL_EINVAL, "bad word-row arguments");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "bit-packed rows need W %% 64 == 0");
+    if (y0 < e->sh.front().y0 || y1 > e->sh.back().y1)
+        return gol_set_error(GOL_EINVAL, "rows [%lld, %lld) are not held by this process", (long long)y0, (long long)y1);
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_load_words(gol_engine *e, int64_t y0, int64_t y1, const uint64_t *words, int64_t stride)
+{
+    RCCHK(rows_check(e, y0, y1, words, stride));
+    if (e->mode == GOL_MODE_EXACT) {  // the loaded bytes' turn 1 is void now: bits[0] holds their 255-cells
+        for (auto &s : e->sh) free_exact_bytes(s);
+        e->mode = GOL_MODE_BITS;
+    }
+    RCCHK(ensure_standard(e));
+    RCCHK(invalidate_halo(e));
+    e->turn = 0;
+    for (auto &s : e->sh) {
+        const int64_t a = std::max(y0, s.y0), b = std::min(y1, s.y1);
+        if (a >= b) continue;
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemcpy2DAsync(s.bits[e->cur] + (a - s.y0) * e->pitch, e->pitch * sizeof(uint32_t), words + (a - y0) * stride,
+                                stride * sizeof(uint64_t), e->W / 8, b - a, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));  // the caller's buffer is only borrowed
+    }
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_store_words(gol_engine *e, int64_t y0, int64_t y1, uint64_t *words, int64_t stride)
+{
+    RCCHK(rows_check(e, y0, y1, words, stride));
+    if (e->mode == GOL_MODE_EXACT)
+        return gol_set_error(GOL_ESTATE, "the board holds bytes other than 0/255 until turn 1: use store_bytes");
+    RCCHK(ensure_standard(e));
+    for (auto &s : e->sh) {
+        const int64_t a = std::max(y0, s.y0), b = std::min(y1, s.y1);
+        if (a >= b) continue;
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemcpy2DAsync(words + (a - y0) * stride, stride * sizeof(uint64_t), s.bits[e->cur] + (a - s.y0) * e->pitch,
+                                e->pitch * sizeof(uint32_t), e->W / 8, b - a, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+    }
+    return GOL_OK;
 }
 
 // ------------------------------------------------------------------ info
@@ -1184,28 +1415,26 @@ extern "C" int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *p
 extern "C" int gol_engine_set_timing(gol_engine *e, int32_t enable)
 {
     if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
+    for (auto &s : e->sh) {  // events of earlier steps may still be pending
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamSynchronize(s.stream));
+    }
     e->timing = enable != 0;
     e->timed.clear();
     for (auto &s : e->sh) s.tused = 0;
+    e->t_ms = e->t_cells = 0;
+    e->t_n = 0;
     return GOL_OK;
 }
 
+// Local (not collective): waits only for this process's timed steps.
 extern "C" int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double *mean_cell_updates)
 {
     if (!e || !launches || !mean_ms || !mean_cell_updates) return gol_set_error(GOL_EINVAL, "bad arguments");
-    RCCHK(sync_all(e));
-    double ms = 0, cells = 0;
-    for (const auto &t : e->timed) {
-        gol_shard &s = e->sh[t.shard];
-        RCCHK(set_dev(s.device));
-        float x = 0;
-        HIPCHK(hipEventElapsedTime(&x, s.tev[t.ev], s.tev[t.ev + 1]));
-        ms += x;
-        cells += t.cell_updates;
-    }
-    const int64_t n = (int64_t)e->timed.size();
+    RCCHK(fold_timing(e));
+    const int64_t n = e->t_n;
     *launches = n;
-    *mean_ms = n ? ms / n : 0.0;
-    *mean_cell_updates = n ? cells / n : 0.0;
+    *mean_ms = n ? e->t_ms / n : 0.0;
+    *mean_cell_updates = n ? e->t_cells / n : 0.0;
     return GOL_OK;
 }

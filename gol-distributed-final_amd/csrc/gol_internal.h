@@ -20,14 +20,19 @@
 // so the kernels address input row y as board + y*pitch for -k <= y < R + k.
 #define GOL_GHOST_ROWS 16
 
+// Timing events per shard before the recorded steps are folded into running sums.
+#define GOL_TIMING_EVENTS 512
+
 // One row shard: rows [y0, y1) of the board on one GPU.
 struct gol_shard {
     int device = 0;
     int64_t y0 = 0, y1 = 0, R = 0;
-    hipStream_t stream = nullptr;  // kernels
+    hipStream_t stream = nullptr;  // kernels (the interior of a step, loads, queries)
+    hipStream_t edge = nullptr;    // the step's launches that read the halo (gol_step_plan)
     hipStream_t comm = nullptr;    // halo exchange
-    hipEvent_t ev_ready = nullptr; // this shard's input board of the next launch is complete
-    hipEvent_t ev_comm = nullptr;  // this shard's halo exchange of the current launch is done
+    hipEvent_t ev_start = nullptr; // a step's inputs are complete and its count slots zeroed
+    hipEvent_t ev_edge = nullptr;  // the rows the next exchange sends are written
+    hipEvent_t ev_halo = nullptr;  // this shard's latest halo exchange is done
     uint32_t *bits[2] = {nullptr, nullptr};        // row 0 of each bit buffer
     uint32_t *bits_alloc[2] = {nullptr, nullptr};  // allocations incl. the ghost rows
     // BYTES mode: the H x W byte board (double buffer).  EXACT mode: bytes[0] = rows
@@ -82,8 +87,14 @@ struct gol_engine {
     int dw = GOL_DEFAULT_DW;
     int band_dw = 4;
     int strip = 0;
+    int kx = 1;                // halo rows of every exchange (>= the k of any step; gol_step_plan)
+    int step_flags = 0;        // GOL_STEP_SERIAL
+    bool halo_ok = false;      // the ghost rows of bits[cur] hold the current halo (kx rows)
+    bool halo_issued = false;  // an exchange was enqueued since the last synchronisation point
     bool timing = false;
     std::vector<gol_timed> timed;
+    double t_ms = 0, t_cells = 0;  // folded timing sums (timed pool recycled)
+    int64_t t_n = 0;
 };
 
 int gol_set_error(int code, const char *fmt, ...);

@@ -12,8 +12,15 @@
 
 // Per-device error word for launches made without one (lazily allocated, zeroed).
 uint32_t *golk_device_err_word(int device);
-// zero the paired-rank claim counters of every stream on `device` (after a faulted launch)
-hipError_t golk_reset_claims(int device);
+// Paired-rank claim counters (one buffer per launch stream, gol_kernels.hip StripMap).
+// golk_reset_claims: zero the buffer of stream s, ordered on s (after a faulted launch).
+// golk_release_claims: free it (the caller has synchronised s; an engine destroying its streams).
+// golk_own_stream: mark s as an engine's stream; golk_reset_claims_device (gol_dev_error, after a
+// fault in a launcher call on a caller's stream) then leaves its buffer alone.
+hipError_t golk_reset_claims(hipStream_t s);
+void golk_release_claims(hipStream_t s);
+void golk_own_stream(hipStream_t s);
+hipError_t golk_reset_claims_device(int device);
 
 int golk_auto_strip(int64_t rows, int64_t ngroups, int k);
 // Standard layout: dw words per lane (1, 2 or 4), k in {1, 2, 4, 8} (and 16 for dw <= 2).

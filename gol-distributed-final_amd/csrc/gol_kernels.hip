@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <set>
 #include <type_traits>
 #include <utility>
 
@@ -2034,17 +2035,55 @@ static uint32_t *claim_counters(hipStream_t s, int cus)
     return c;
 }
 
-hipError_t golk_reset_claims(int device)
+static std::set<hipStream_t> engine_streams;  // streams owned by an engine (golk_own_stream)
+
+hipError_t golk_reset_claims(hipStream_t s)
+{
+    std::lock_guard<std::mutex> lock(claims_mu);
+    hipError_t e = hipSuccess;
+    for (auto &kv : claims_bufs) {
+        if (kv.first.first != s) continue;
+        int cus = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, kv.first.second);
+        if (e == hipSuccess) e = hipMemsetAsync(kv.second, 0, claims_bytes(cus), s);  // before any later launch on s
+        if (e != hipSuccess) break;
+    }
+    return e;
+}
+
+void golk_release_claims(hipStream_t s)
+{
+    std::lock_guard<std::mutex> lock(claims_mu);
+    for (auto it = claims_bufs.begin(); it != claims_bufs.end();) {
+        if (it->first.first == s) {
+            (void)hipFree(it->second);
+            it = claims_bufs.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    engine_streams.erase(s);
+}
+
+void golk_own_stream(hipStream_t s)
+{
+    std::lock_guard<std::mutex> lock(claims_mu);
+    engine_streams.insert(s);
+}
+
+hipError_t golk_reset_claims_device(int device)
 {
     std::lock_guard<std::mutex> lock(claims_mu);
     int cus = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    bool any = false;
     for (auto &kv : claims_bufs) {
         if (e != hipSuccess) break;
-        if (kv.first.second != device) continue;
-        e = hipMemset(kv.second, 0, claims_bytes(cus));
+        if (kv.first.second != device || engine_streams.count(kv.first.first)) continue;
+        e = hipMemsetAsync(kv.second, 0, claims_bytes(cus), kv.first.first);
+        any = true;
     }
-    if (e == hipSuccess) e = hipDeviceSynchronize();  // the zeroes land before any later launch
+    if (e == hipSuccess && any) e = hipDeviceSynchronize();  // gol_dev_error is synchronous
     return e;
 }
 

@@ -3,13 +3,14 @@
 * ``Engine``               one GPU, board resident in HBM (gol_engine_*)
 * ``Operations``           broker RPC service mirror (broker.go:62-277)
 * ``GameOfLifeOperations`` worker RPC service mirror (worker.go:73-86)
-* ``ShardedBoard``         row-sharded torus, one process per GPU, RCCL halo exchange
+* ``ShardedBoard``         torch.distributed mirror of the sharded step (runs the library's plans)
+* ``halo_plan`` / ``step_plan``  the sharded step's schedule as data (gol_halo_plan, gol_step_plan)
 * ``distributor``          controller mirror (gol/gol.go + gol/distributor.go) over the broker API
 * ``next_state_slab`` / ``partition_rows``  worker.go:15-70 / broker.go:135-206
 
 Everything runs through libgolhip.so (hipcc, gfx950); there is no CPU fallback.
 """
-from ._lib import GolError, device_count, lib  # noqa: F401
+from ._lib import GolError, device_count, halo_plan, lib, step_plan  # noqa: F401
 from .broker import Operations  # noqa: F401
 from .engine import Engine, next_state_slab, partition_rows  # noqa: F401
 from .pgm import read_pgm, write_pgm_bytes  # noqa: F401

@@ -29,6 +29,9 @@ GOL_TRANSPORT_AUTO, GOL_TRANSPORT_LOOPBACK, GOL_TRANSPORT_RCCL, GOL_TRANSPORT_LO
 TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "rccl": GOL_TRANSPORT_RCCL}
 TRANSPORT_NAMES = {GOL_TRANSPORT_LOOPBACK: "loopback", GOL_TRANSPORT_RCCL: "rccl", GOL_TRANSPORT_LOCAL: "local"}
 GOL_SHARDS_SAME_DEVICE = 1
+GOL_STEP_SERIAL = 2
+GOL_HALO_SEND, GOL_HALO_RECV = 0, 1
+GOL_LAUNCH_MAIN, GOL_LAUNCH_EDGE = 0, 1
 
 _NAMES = {
     GOL_EINVAL: "EINVAL", GOL_EHIP: "EHIP", GOL_ENOMEM: "ENOMEM", GOL_EIO: "EIO",
@@ -64,6 +67,19 @@ class gol_response(ctypes.Structure):
                 ("work_stride", ctypes.c_int64), ("Worker", ctypes.c_int64)]
 
 
+# int (*gol_write_fn)(void *user, int64_t offset, const uint8_t *data, int64_t len)
+GOL_WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64)
+
+
+class gol_halo_op(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("row", ctypes.c_int64), ("rows", ctypes.c_int64)]
+
+
+class gol_launch(ctypes.Structure):
+    _fields_ = [("stream", ctypes.c_int32), ("needs_halo", ctypes.c_int32), ("row0", ctypes.c_int64),
+                ("rows", ctypes.c_int64)]
+
+
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
 _u64 = ctypes.c_uint64
@@ -95,11 +111,16 @@ SIGNATURES = [
     ("gol_engine_alive_cells", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
     ("gol_engine_step_flips", ctypes.c_int, [_vp, _vp, _i64, _P(_i64)]),
     ("gol_engine_write_pgm", ctypes.c_int, [_vp, ctypes.c_char_p]),
+    ("gol_engine_write_pgm_to", ctypes.c_int, [_vp, _vp, _vp]),
+    ("gol_engine_load_words", ctypes.c_int, [_vp, _i64, _i64, _vp, _i64]),
+    ("gol_engine_store_words", ctypes.c_int, [_vp, _i64, _i64, _vp, _i64]),
     ("gol_engine_hash", ctypes.c_int, [_vp, _P(_u64)]),
     ("gol_engine_info", ctypes.c_int, [_vp, _P(_i32), _P(_i32), _P(_i32), _P(_i32)]),
     ("gol_engine_device_bits", ctypes.c_int, [_vp, _P(_vp), _P(_i64)]),
     ("gol_engine_set_timing", ctypes.c_int, [_vp, _i32]),
     ("gol_engine_timing", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double), _P(ctypes.c_double)]),
+    ("gol_halo_plan", ctypes.c_int, [_i64, _i32, _i32, _i32, _P(gol_halo_op), _i32, _P(_i32)]),
+    ("gol_step_plan", ctypes.c_int, [_i64, _i32, _i32, _i32, _P(gol_launch), _i32, _P(_i32)]),
     ("gol_dev_bits_step", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp]),
     ("gol_dev_random_fill", ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _u64, _vp]),
@@ -165,6 +186,25 @@ def lib():
 def check(rc: int) -> None:
     if rc != GOL_OK:
         raise GolError(rc, lib().gol_last_error().decode(errors="replace"))
+
+
+def halo_plan(H: int, nranks: int, rank: int, k: int) -> list[tuple[str, int, int, int]]:
+    """gol_halo_plan: the halo exchange of `rank` in issue order, as (kind "send"/"recv", peer,
+    first shard-local row, rows).  Host code: no GPU needed."""
+    ops = (gol_halo_op * 4)()
+    n = ctypes.c_int32()
+    check(lib().gol_halo_plan(H, nranks, rank, k, ops, 4, ctypes.byref(n)))
+    return [("send" if o.kind == GOL_HALO_SEND else "recv", o.peer, o.row, o.rows) for o in ops[:n.value]]
+
+
+def step_plan(R: int, k: int, kx: int, serial: bool = False) -> list[tuple[str, bool, int, int]]:
+    """gol_step_plan: the launches of one k-turn step of an R-row shard, as (stream "main"/"edge",
+    needs_halo, first output row, rows)."""
+    out = (gol_launch * 3)()
+    n = ctypes.c_int32()
+    check(lib().gol_step_plan(R, k, kx, GOL_STEP_SERIAL if serial else 0, out, 3, ctypes.byref(n)))
+    return [("edge" if L.stream == GOL_LAUNCH_EDGE else "main", bool(L.needs_halo), L.row0, L.rows)
+            for L in out[:n.value]]
 
 
 def device_count() -> int:

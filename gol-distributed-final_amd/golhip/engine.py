@@ -14,8 +14,8 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, LAYOUTS, TRANSPORT_NAMES, TRANSPORTS, GolError,
-                   check, gol_config, lib)
+from ._lib import (GOL_RCCL_ID_BYTES, GOL_WRITE_FN, GOL_SHARDS_SAME_DEVICE, GOL_STEP_SERIAL, LAYOUTS, TRANSPORT_NAMES, TRANSPORTS,
+                   GolError, check, gol_config, lib)
 
 
 def rccl_unique_id(library=None) -> bytes:
@@ -31,12 +31,14 @@ def rccl_unique_id(library=None) -> bytes:
 class Engine:
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
                  strip_rows: int = 0, device: int = -1, layout: str = "auto", shards: int = 1,
-                 transport: str = "auto", same_device: bool = False, library=None, _rank=None):
+                 transport: str = "auto", same_device: bool = False, serial_step: bool = False, library=None,
+                 _rank=None):
         self.H, self.W = int(height), int(width)
         self._L = library or lib()
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, strip_rows=strip_rows,
                          cells_per_lane=cells_per_lane, layout=LAYOUTS[layout], shards=shards,
-                         transport=TRANSPORTS[transport], flags=GOL_SHARDS_SAME_DEVICE if same_device else 0)
+                         transport=TRANSPORTS[transport],
+                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | (GOL_STEP_SERIAL if serial_step else 0))
         h = ctypes.c_void_p()
         if _rank is None:
             self._check(self._L.gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))
@@ -101,6 +103,37 @@ class Engine:
 
     def write_pgm(self, path: str) -> None:
         self._check(self._L.gol_engine_write_pgm(self._h, path.encode()))
+
+    def write_pgm_to(self, sink) -> None:
+        """The P5 byte stream (gol/io.go:52-81) into sink(offset, memoryview) instead of a file:
+        the header, then chunks of rows in row order (this process's rows, at their file
+        offsets).  The memoryview is only valid during the call."""
+        err = []
+
+        def cb(_user, off, data, n):
+            try:
+                sink(off, (ctypes.c_uint8 * n).from_address(data))
+                return 0
+            except BaseException as x:  # noqa: BLE001 -- reported after the call
+                err.append(x)
+                return 1
+        fn = GOL_WRITE_FN(cb)
+        rc = self._L.gol_engine_write_pgm_to(self._h, fn, None)
+        if err:
+            raise err[0]
+        self._check(rc)
+
+    def load_words(self, y0: int, words: np.ndarray) -> None:
+        """Rows [y0, y0 + len(words)) from bit-packed uint64 rows (64 cells per word, LSB = lowest x)."""
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        if words.ndim != 2 or words.shape[1] != self.W // 64:
+            raise ValueError(f"expected (rows, {self.W // 64}) uint64 words")
+        self._check(self._L.gol_engine_load_words(self._h, y0, y0 + words.shape[0], words.ctypes.data, words.shape[1]))
+
+    def store_words(self, y0: int, y1: int) -> np.ndarray:
+        out = np.empty((max(y1 - y0, 0), self.W // 64), dtype=np.uint64)
+        self._check(self._L.gol_engine_store_words(self._h, y0, y1, out.ctypes.data, self.W // 64))
+        return out
 
     # -- stepping and queries
     def step(self, turns: int) -> None:
@@ -170,7 +203,7 @@ class Engine:
         self._check(self._L.gol_engine_set_timing(self._h, 1 if enable else 0))
 
     def timing(self) -> dict:
-        """HIP-event timing of the step-kernel launches since set_timing(True)."""
+        """HIP-event timing of every shard-step since set_timing(True) (edge launches included)."""
         n, ms, cells = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
         self._check(self._L.gol_engine_timing(self._h, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(cells)))
         return {"launches": n.value, "mean_ms": ms.value, "mean_cell_updates": cells.value}

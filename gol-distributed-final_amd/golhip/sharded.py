@@ -1,22 +1,20 @@
-"""Row-sharded Game-of-Life torus over several MI355X, one process per GPU.
+"""torch.distributed mirror of the row-sharded step -- one process per rank.
 
-The reference splits the board into `Threads` row slabs per turn and ships the
-WHOLE board to every worker each turn (broker.go:135-206, 143-157).  Here the
-same partition (gol_partition_rows, broker.go:172-206) is applied once to GPUs:
-rank r keeps rows [y0_r, y1_r) bit-packed in its own HBM for the whole run.
-Every k turns the only traffic is a k-row halo with each ring neighbour,
-exchanged with torch.distributed point-to-point ops (backend "nccl" = RCCL
-over xGMI on MI355X) while the interior rows are computed:
+The product's sharded board is libgolhip.so's engine (gol_engine_create_rank: RCCL halo
+exchange inside the library, golhip.Engine.rank).  This module runs the SAME schedule with
+torch.distributed point-to-point ops, so that it can be driven on the CPU with the gloo
+backend (tests/test_sharded_gloo.py) or with several ranks sharing one GPU: the halo plan
+(gol_halo_plan) and the step plan (gol_step_plan) come from the library, not from here.
 
-    isend(my top k rows -> rank-1)   irecv(bottom halo <- rank+1)
-    isend(my bottom k rows -> rank+1) irecv(top halo   <- rank-1)
-    interior launch: output rows [k, R-k)      (needs no halo; overlaps the exchange)
-    wait; boundary launches: rows [0, k) and [R-k, R)
+The reference splits the board into `Threads` row slabs per turn and ships the WHOLE board
+to every worker each turn (broker.go:135-206, 143-157).  Here the partition
+(gol_partition_rows, broker.go:172-206) is applied once: rank r keeps rows [y0_r, y1_r) and,
+per k-turn step, computes the edge rows (which read the kmax halo rows) and the interior,
+then exchanges the new edge rows with its ring neighbours.
 
-With one rank there is no exchange: the kernel reads the torus wrap directly.
-Counts and hashes are per-shard reductions summed with one all_reduce.
-PyTorch provides device memory, the stream and torch.distributed only; all
-board arithmetic runs in libgolhip.so's gfx950 kernels.
+Counts and hashes are per-shard reductions summed with one all_reduce.  PyTorch provides
+device memory, the stream and torch.distributed only; all board arithmetic runs in
+libgolhip.so's gfx950 kernels (or, in the CPU tests, an oracle stand-in).
 """
 from __future__ import annotations
 
@@ -26,7 +24,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ._lib import GOL_COUNT_SLOTS, check, lib
+from ._lib import GOL_COUNT_SLOTS, check, halo_plan, lib, step_plan
 from .engine import partition_rows
 
 VALID_K = (16, 12, 8, 4, 2, 1)
@@ -136,11 +134,10 @@ class ShardedBoard:
         self._store = [torch.zeros((self.R + 2 * self.kmax, self.pitch), **z) for _ in range(2)]
         self.buf = [t[self.kmax:self.kmax + self.R] for t in self._store]
         self.cur = 0
+        self.halo_ok = False  # the ghost rows of buf[cur] hold the current halo (kmax rows)
         self.slots = torch.zeros(GOL_COUNT_SLOTS * 8, dtype=torch.int64, device=self.device)
         self.turn = 0
-        self.prev = (self.rank - 1) % self.nranks
-        self.next = (self.rank + 1) % self.nranks
-        # per-launch timing hooks for bench.py: called as hook("interior"|"boundary"|"full", k, rows)
+        # per-launch hooks (tests): called as hook("edge"|"main", k, rows, before)
         self.launch_hook = None
 
     # ------------------------------------------------------------ board in/out
@@ -152,6 +149,7 @@ class ShardedBoard:
         """Synthetic torus: identical global board for every rank count."""
         self.kern.random_fill(self.board, self.y0, self.W, seed)
         self.band = False
+        self.halo_ok = False
         self.turn = 0
 
     def _convert(self, to_band: bool) -> None:
@@ -159,6 +157,7 @@ class ShardedBoard:
             return
         self.kern.band_convert(to_band, self.board, self.buf[1 - self.cur])
         self.cur = 1 - self.cur
+        self.halo_ok = False
         self.band = to_band
 
     def standard(self) -> torch.Tensor:
@@ -172,6 +171,7 @@ class ShardedBoard:
             raise ValueError("expected this rank's (R, W) rows")
         self.kern.pack(board_rows.to(self.device).contiguous(), self.board)
         self.band = False
+        self.halo_ok = False
         self.turn = 0
 
     def load_pgm(self, path: str, chunk_rows: int = 4096) -> None:
@@ -189,6 +189,7 @@ class ShardedBoard:
         if int(flag.item()):
             raise ValueError(f"{path}: bytes other than 0/255 (use the single-GPU engine for those)")
         self.band = False
+        self.halo_ok = False
         self.turn = 0
 
     # ------------------------------------------------------------ stepping
@@ -197,32 +198,44 @@ class ShardedBoard:
         st, km, R = self._store[self.cur], self.kmax, self.R
         return st[km - k:km], st[km + R:km + R + k]
 
-    def _exchange(self, k: int):
-        cur = self.board
-        top_h, bot_h = self.halo(k)
+    def _rows(self, row: int, rows: int) -> torch.Tensor:
+        """Shard-local rows [row, row + rows) of buf[cur], ghost rows (row < 0 or >= R) included."""
+        return self._store[self.cur][self.kmax + row:self.kmax + row + rows]
+
+    def _exchange(self) -> None:
+        """The library's halo plan (gol_halo_plan, the schedule libgolhip.so's engine runs) for
+        this rank, kmax rows each way, in its issue order as torch.distributed P2P ops: a
+        receiver's n-th receive from a peer meets that peer's n-th send to it (for two ranks one
+        peer on both sides).  One rank: the plan's sends to itself, paired the same way (the
+        torus wrap)."""
+        plan = halo_plan(self.H, self.nranks, self.rank, self.kmax)
         if self.nranks == 1:
-            # torus wrap: the last k rows above row 0, the first k rows below row R-1
-            top_h.copy_(cur[self.R - k:])
-            bot_h.copy_(cur[:k])
-            return []
+            sends = [self._rows(row, n).clone() for kind, _, row, n in plan if kind == "send"]
+            recvs = [(row, n) for kind, _, row, n in plan if kind == "recv"]
+            for (row, n), src in zip(recvs, sends):
+                self._rows(row, n).copy_(src)
+            return
         g = self.group
-        if self.device.type == "cuda" and dist.get_backend(g) == "gloo":
-            # gloo has no device P2P: stage the halo rows through host memory (used to test
-            # several ranks sharing one GPU; production runs use nccl = RCCL over xGMI).
-            up, down = cur[:k].cpu(), cur[self.R - k:].cpu()
-            bot, top = torch.empty_like(up), torch.empty_like(down)
-            ops = [dist.P2POp(dist.isend, up, self.prev, g), dist.P2POp(dist.irecv, bot, self.next, g),
-                   dist.P2POp(dist.isend, down, self.next, g), dist.P2POp(dist.irecv, top, self.prev, g)]
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
-            bot_h.copy_(bot)
-            top_h.copy_(top)
-            return []
-        ops = [dist.P2POp(dist.isend, cur[:k], self.prev, g),
-               dist.P2POp(dist.irecv, bot_h, self.next, g),
-               dist.P2POp(dist.isend, cur[self.R - k:], self.next, g),
-               dist.P2POp(dist.irecv, top_h, self.prev, g)]
-        return dist.batch_isend_irecv(ops)
+        stage = self.device.type == "cuda" and dist.get_backend(g) == "gloo"
+        ops, land = [], []
+        for kind, peer, row, n in plan:
+            t = self._rows(row, n)
+            if stage:
+                # gloo has no device P2P: stage the halo rows through host memory (several ranks
+                # sharing one GPU in tests; production runs RCCL inside libgolhip.so)
+                buf = t.cpu() if kind == "send" else torch.empty(t.shape, dtype=t.dtype)
+                if kind == "recv":
+                    land.append((t, buf))
+                t = buf
+            elif kind == "recv" and not t.is_contiguous():
+                buf = torch.empty_like(t)
+                land.append((t, buf))
+                t = buf
+            ops.append(dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer, g))
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        for dst, buf in land:
+            dst.copy_(buf)
 
     def _launch(self, kind, top, bot, dst, row0, rows, k, slots):
         if rows <= 0:
@@ -236,9 +249,13 @@ class ShardedBoard:
             hook(kind, k, rows, False)
 
     def step(self, turns: int, count: bool = False) -> None:
-        """Advance exactly `turns` turns (k-turn launches + halo exchange)."""
+        """Advance exactly `turns` turns: per k-turn step the launches of the library's step plan
+        (gol_step_plan: the edge rows, which read the halo, and the interior), then the next
+        step's halo exchange (gol_halo_plan, kmax rows)."""
         if turns > 0 and self.use_band:
             self._convert(True)
+        if turns > 0 and not self.halo_ok:
+            self._exchange()
         while turns > 0:
             k = max(kk for kk in self.valid_k if kk <= min(self.kmax, turns))
             last = turns == k
@@ -246,23 +263,12 @@ class ShardedBoard:
             if slots is not None:
                 slots.zero_()
             dst = self.buf[1 - self.cur]
-            R = self.R
             top, bot = self.halo(k)
-            reqs = self._exchange(k)
-            if self.nranks == 1:
-                self._launch("full", top, bot, dst, 0, R, k, slots)
-            else:
-                interior = R >= 3 * k
-                if interior:  # rows [k, R-k) need no halo: overlaps the exchange
-                    self._launch("interior", top, bot, dst, k, R - 2 * k, k, slots)
-                for r in reqs:
-                    r.wait()
-                if interior:
-                    self._launch("boundary", top, bot, dst, 0, k, k, slots)
-                    self._launch("boundary", top, bot, dst, R - k, k, k, slots)
-                else:
-                    self._launch("boundary", top, bot, dst, 0, R, k, slots)
+            for stream, _, row0, rows in step_plan(self.R, k, self.kmax):
+                self._launch("edge" if stream == "edge" else "main", top, bot, dst, row0, rows, k, slots)
             self.cur = 1 - self.cur
+            self._exchange()
+            self.halo_ok = True
             self.turn += k
             turns -= k
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GOL_ABI_VERSION 2
+#define GOL_ABI_VERSION 3
 
 enum {
     GOL_OK = 0,
@@ -80,11 +80,14 @@ int gol_partition_rows(int64_t H, int64_t parts, int64_t i, int64_t *y0, int64_t
  *
  * Row sharding (broker.go:135-206 applied to GPUs): the board's rows are split
  * with gol_partition_rows over `nranks` shards; shard r keeps rows
- * [y0_r, y1_r) plus 16 ghost rows above and below.  Before every k-turn
- * launch each shard receives the k rows above it from shard r-1 and the k rows
- * below it from shard r+1 (mod nranks) into its ghost rows, while the interior
- * rows [k, R-k), which need no halo, are already being computed; the boundary
- * rows follow once the halo is in.  k <= min shard rows.
+ * [y0_r, y1_r) plus 16 ghost rows above and below.  Every k-turn step needs in
+ * its ghost rows the k rows above the shard (from shard r-1) and below it
+ * (from shard r+1, mod nranks): gol_halo_plan.  A step first computes the kx
+ * rows at each edge of the shard (they read the halo) and, beside them, the
+ * interior; the next step's halo is exchanged as soon as the edge rows are
+ * written, while the interior is still running (gol_step_plan).  One shard
+ * (the whole torus) runs the same step with its own rows as the halo.
+ * k <= kx <= min shard rows.
  *  - one process, `shards` local shards (gol_config.shards): GPUs device,
  *    device+1, ... (or all on `device` with GOL_SHARDS_SAME_DEVICE);
  *  - one process per GPU (gol_engine_create_rank): this process holds shard
@@ -110,6 +113,7 @@ typedef struct gol_engine gol_engine;
 #define GOL_TRANSPORT_LOCAL 3    /* (reported only) one shard, wrap rows copied on its own stream */
 /* gol_config.flags */
 #define GOL_SHARDS_SAME_DEVICE 1 /* every local shard on `device` (loopback testing on one GPU) */
+#define GOL_STEP_SERIAL 2        /* one launch per shard and step, after the halo exchange (gol_step_plan) */
 typedef struct gol_config {
     int32_t device;           /* HIP device ordinal (first shard); -1 = current device */
     int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
@@ -183,6 +187,23 @@ int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n);
  * bytes, streamed from the device in chunks; with several processes every
  * rank writes its own rows at their offset (collective). */
 int gol_engine_write_pgm(gol_engine *e, const char *path);
+/* The same byte stream handed to a caller's sink instead of a file (a pipe,
+ * a socket, a hash, a compressor: config 5's 2^20 x 2^20 board is 1 TiB as
+ * P5).  The sink gets (user, file offset, bytes, length) for the header and
+ * then every chunk of rows (at most 64 MiB each) of the shards of this process
+ * in row order, and returns 0 (nonzero aborts the write with GOL_EIO).  With
+ * ranks in several processes every rank calls it (collective) and its sink
+ * sees its own rows at their offsets; rank 0's also gets the header. */
+typedef int (*gol_write_fn)(void *user, int64_t offset, const uint8_t *data, int64_t len);
+int gol_engine_write_pgm_to(gol_engine *e, gol_write_fn sink, void *user);
+/* Bit-packed rows [y0, y1) (global, held by this process) in or out: 64 cells
+ * per uint64 (LSB = lowest x), `stride` uint64 words per row, W % 64 == 0.
+ * load_words overwrites those rows of the current board (several calls may
+ * load a board piece by piece), resets the turn counter to 0.  store_words
+ * reads them (GOL_ESTATE before turn 1 of a board loaded with bytes other than
+ * 0/255: use store_bytes).  One eighth of the PCIe traffic of the byte calls. */
+int gol_engine_load_words(gol_engine *e, int64_t y0, int64_t y1, const uint64_t *words, int64_t stride);
+int gol_engine_store_words(gol_engine *e, int64_t y0, int64_t y1, uint64_t *words, int64_t stride);
 /* Order-independent board hash (same definition as oracle_hash_words):
  * sum over 64-bit words of splitmix64(word ^ splitmix64(y*W/64 + w)).
  * W % 64 == 0 only. */
@@ -194,13 +215,55 @@ int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lane, int32_t 
 /* Raw device pointer to the current bit board of local shard 0 (pitch in
  * uint32 words), for tests. */
 int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *pitch);
-/* Kernel timing: with timing on, HIP events on the launching stream bracket
- * every launch of the step kernel over a shard's interior rows (or all its
- * rows when it has no separate interior launch).  gol_engine_timing returns
- * the number of timed launches since timing was (re)enabled, their mean
- * duration and their mean cell-updates (rows x W x k). */
+/* Step timing: with timing on, HIP events on each shard's compute stream
+ * bracket every k-turn step of the shard: from before its first launch to the
+ * end of its last one, the edge launches included (gol_step_plan).
+ * gol_engine_timing returns the number of timed shard-steps since timing was
+ * (re)enabled, their mean duration and their mean cell-updates (R x W x k). */
 int gol_engine_set_timing(gol_engine *e, int32_t enable);
 int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double *mean_cell_updates);
+
+/* ---------------------------------------------------------------- plans
+ * The schedule of a sharded step as data (host functions, no GPU needed).  The
+ * engine runs exactly these plans; golhip.sharded (the torch.distributed
+ * mirror) and the tests read them.  Replaces the broker's per-turn fan-out
+ * (broker.go:135-206: every worker gets the whole board) by a k-row halo with
+ * the ring neighbours.
+ *
+ * gol_halo_plan: the halo exchange of global rank `rank` of an H-row board
+ * split over nranks shards (gol_partition_rows), k rows each way, in issue
+ * order.  Sends read shard-local rows [row, row + rows) of the shard, receives
+ * write its ghost rows [row, row + rows) (row = -k or R).  A receiver matches
+ * the sends addressed to it by one sender with its receives from that sender
+ * in issue order (ncclSend/ncclRecv semantics; for nranks = 2 both neighbours
+ * are one peer, for nranks = 1 the shard sends to itself: the torus wrap).
+ * Writes min(4, cap) ops; *n = 4. */
+#define GOL_HALO_SEND 0
+#define GOL_HALO_RECV 1
+typedef struct gol_halo_op {
+    int32_t kind;  /* GOL_HALO_SEND / GOL_HALO_RECV */
+    int32_t peer;  /* global rank of the other side */
+    int64_t row;   /* first shard-local row of the block */
+    int64_t rows;  /* k */
+} gol_halo_op;
+int gol_halo_plan(int64_t H, int32_t nranks, int32_t rank, int32_t k, gol_halo_op *ops, int32_t cap, int32_t *n);
+/* gol_step_plan: the launches of one k-turn step of a shard of R rows whose
+ * halo exchanges carry kx >= k rows.  EDGE launches run on the shard's edge
+ * stream once the halo is in; MAIN launches on its compute stream.  With
+ * R >= 3 kx (and no GOL_STEP_SERIAL): rows [0, kx) and [R - kx, R) on the edge
+ * stream, the interior [kx, R - kx) (it reads no ghost row) on the compute
+ * stream beside them, and the next step's exchange starts when the edge rows
+ * are written.  Otherwise one MAIN launch over [0, R) after the halo.  Writes
+ * min(n, cap) launches. */
+#define GOL_LAUNCH_MAIN 0
+#define GOL_LAUNCH_EDGE 1
+typedef struct gol_launch {
+    int32_t stream;     /* GOL_LAUNCH_MAIN / GOL_LAUNCH_EDGE */
+    int32_t needs_halo; /* reads the ghost rows: waits for the exchange */
+    int64_t row0;       /* first shard-local output row */
+    int64_t rows;
+} gol_launch;
+int gol_step_plan(int64_t R, int32_t k, int32_t kx, int32_t flags, gol_launch *out, int32_t cap, int32_t *n);
 
 /* ---------------------------------------------------------------- device launchers
  * Asynchronous kernel launches on caller-owned device memory and a caller

@@ -1,0 +1,173 @@
+"""Every BASELINE.json configuration at its own size, through golhip.Engine -- the engine
+path bench.py times -- against the oracle.
+
+The oracle cannot run boards of 2^32..2^40 cells, so the big boards are tori TILED with a
+small random torus: a torus tiled with copies of a th x tw torus evolves exactly as the
+small torus does (every neighbourhood is a neighbourhood of the small torus), so every
+tile of the big board must equal the oracle's small-board result, bit for bit, and every
+alive count must be the small count times the number of tiles.  Boards are loaded and read
+as bit-packed rows (gol_engine_load_words / store_words).  The random bench board itself is
+checked against a second, independent kernel family (the standard-layout k = 1 step).
+
+  config 3  65536^2, k = 12 band pipeline (one round, paired ranges)    test_config3_*
+  config 4  262144^2 on one GPU, and as 2 shards of that GPU            test_config4_*
+  config 5  the bench's 2^17 x 2^20 per-GPU shard, exact bench workload test_config5_bench_*
+            the whole 2^20 x 2^20 torus on one GPU, counts every 10
+            turns and the P5 snapshot streamed to a sink                test_config5_full_*
+(config 1 and 2 at size: tests/test_gpu_engine.py.)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def G():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import golhip
+    golhip.lib()
+    return golhip
+
+
+def _tile(seed, th, tw, turns, every):
+    """A random th x tw torus (uint64 words) and the oracle's result and counts after `turns`."""
+    words = O.random_words(seed, 0, th, tw // 64)
+    ref, counts = O.bits_run(words, turns, with_counts=True)
+    return words, ref, [int(c) for c in counts[every - 1::every]]
+
+
+def _load_tiled(e, H, W, tile, chunk_rows=8192):
+    th, tww = tile.shape
+    assert H % th == 0 and W % (64 * tww) == 0 and chunk_rows % th == 0
+    block = np.tile(tile, (chunk_rows // th, W // 64 // tww))
+    for y in range(0, H, chunk_rows):
+        n = min(chunk_rows, H - y)
+        e.load_words(y, block[:n])
+
+
+def _check_tiled(e, H, W, ref, chunk_rows=8192):
+    th, tww = ref.shape
+    for y in range(0, H, chunk_rows):
+        n = min(chunk_rows, H - y)
+        got = e.store_words(y, y + n).reshape(n // th, th, W // 64 // tww, tww)
+        assert (got == ref[None, :, None, :]).all(), f"rows [{y}, {y + n})"
+
+
+def _free_engine(e):
+    import torch
+    e.close()
+    torch.cuda.empty_cache()
+
+
+def test_config3_65536_tiled(G):
+    """65536^2 (config 3): two k = 12 launches with the count fused into each (the bench's
+    step), a 1-turn launch, then the whole board against the oracle's 256 x 1024 tile."""
+    H = W = 65536
+    tile, ref, counts = _tile(31, 256, 1024, 25, 12)
+    reps = (H // 256) * (W // 1024)
+    with G.Engine(H, W, device=0) as e:
+        info = e.info()
+        assert info["layout"] == "band" and info["turns_per_launch"] == 12
+        _load_tiled(e, H, W, tile)
+        got = e.step_counted(24, 12)
+        assert got.tolist() == [reps * c for c in counts]
+        e.step(1)
+        _check_tiled(e, H, W, ref)
+        assert e.alive_count() == reps * O.popcount_words(ref)
+
+
+def test_config4_262144_full_board(G):
+    """262144^2 (config 4) on one GPU (8 GiB per buffer): 24 turns in two counted k = 12
+    launches, every tile against the oracle; then the same board as 2 row shards of the same
+    GPU (loopback halo plan) gives the same hash and counts."""
+    H = W = 262144
+    tile, ref, counts = _tile(41, 512, 2048, 24, 12)
+    reps = (H // 512) * (W // 2048)
+    with G.Engine(H, W, device=0) as e:
+        _load_tiled(e, H, W, tile)
+        assert e.step_counted(24, 12).tolist() == [reps * c for c in counts]
+        _check_tiled(e, H, W, ref, chunk_rows=16384)
+        h1 = e.hash()
+        _free_engine(e)
+    with G.Engine(H, W, device=0, shards=2, same_device=True, transport="loopback") as e:
+        _load_tiled(e, H, W, tile)
+        assert e.step_counted(24, 12).tolist() == [reps * c for c in counts]
+        assert e.hash() == h1
+        _free_engine(e)
+
+
+def test_config5_bench_workload_exact(G):
+    """The bench's exact workload (bench.py, default: seed 1, 2^17 x 2^20, 5 warm-up + 20 timed
+    k = 12 launches, the count fused into every launch): the 25 counts and the final hash equal a
+    run of the independent standard-layout k = 1 kernel counted every 12 turns, and the last
+    count is the `alive_final` of the driver's BENCH line."""
+    H, W = 1 << 17, 1 << 20
+    with G.Engine(H, W, device=0) as e:
+        assert e.info()["turns_per_launch"] == 12 and e.info()["layout"] == "band"
+        e.load_random(1)
+        band = e.step_counted(5 * 12, 12).tolist() + e.step_counted(20 * 12, 12).tolist()
+        h_band = e.hash()
+        _free_engine(e)
+    with G.Engine(H, W, device=0, layout="standard", turns_per_launch=1) as e:
+        assert e.info()["turns_per_launch"] == 1
+        e.load_random(1)
+        std = e.step_counted(300, 12).tolist()
+        h_std = e.hash()
+        _free_engine(e)
+    assert band == std
+    assert h_band == h_std
+    assert band[-1] == 8848272907  # BENCH_r02.json config.alive_final (turn 300)
+
+
+@pytest.mark.timeout(600)
+def test_config5_full_board_one_gpu(G):
+    """The whole 2^20 x 2^20 torus of config 5 on ONE GPU (2 x 128 GiB of the 288 GB HBM): 30
+    turns with the alive count every 10 turns (distributor.go:39-51's AliveCellsCount, fused on
+    the GPU), every count against the oracle's tile, then the P5 snapshot (io.go:42-87, 1 TiB)
+    streamed through gol_engine_write_pgm_to into a sink that checks the header, the offsets
+    and every 97th chunk of rows byte for byte against the oracle's tile."""
+    import torch
+    H = W = 1 << 20
+    th, tw = 256, 1024
+    tile, ref, counts = _tile(51, th, tw, 30, 10)
+    reps = (H // th) * (W // tw)
+    try:
+        e = G.Engine(H, W, device=0)
+    except G.GolError as x:
+        free, total = torch.cuda.mem_get_info(0)
+        pytest.skip(f"2^20 x 2^20 does not fit: {x} (free {free / 2**30:.1f} of {total / 2**30:.1f} GiB)")
+    try:
+        _load_tiled(e, H, W, tile, chunk_rows=4096)
+        assert e.step_counted(30, 10).tolist() == [reps * c for c in counts]
+        assert e.alive_count() == reps * O.popcount_words(ref)
+        ref_rows = O.unpack(ref)  # th x tw bytes, 0 / 255
+        header = b"P5\n%d %d\n255\n" % (W, H)
+        seen = {"next": 0, "chunks": 0, "checked": 0}
+
+        def sink(off, buf):
+            assert off == seen["next"], (off, seen["next"])
+            n = len(buf)
+            if off == 0:
+                assert bytes(buf) == header
+            else:
+                assert (off - len(header)) % W == 0 and n % W == 0
+                if seen["chunks"] % 97 == 0:
+                    y = (off - len(header)) // W
+                    got = np.frombuffer(buf, dtype=np.uint8).reshape(n // W, W // tw, tw)
+                    want = ref_rows[np.arange(y, y + n // W) % th]
+                    assert (got == want[:, None, :]).all(), f"rows at {y}"
+                    seen["checked"] += 1
+                seen["chunks"] += 1
+            seen["next"] = off + n
+        e.write_pgm_to(sink)
+        assert seen["next"] == len(header) + H * W
+        assert seen["checked"] > 100
+    finally:
+        _free_engine(e)

@@ -328,24 +328,20 @@ def test_tiled_board_matches_small_torus(golhip):
         assert e.alive_count() == reps_y * reps_x * int(np.count_nonzero(ref))
 
 
-def test_bench_size_k_and_shard_invariance(golhip):
-    """2^17 x 2^20 (the bench's per-GPU torus): k=1, 8 and 16 launches on the standard layout
-    and k=1, 8 on the band layout give the same board hash, and the fused popcount equals the
-    popcount kernel."""
+def test_bench_size_k_and_layout_invariance(golhip):
+    """2^17 x 2^20 (the bench's per-GPU torus) through the engine: k=1, 8 and 16 launches on the
+    standard layout and k=1, 8 and 12 on the band layout give the same board hash, and the count
+    fused into the last launch equals the popcount kernel."""
     import torch
-    from golhip.sharded import ShardedBoard
-    H, W, turns = 1 << 17, 1 << 20, 16
+    H, W, turns = 1 << 17, 1 << 20, 48
     hashes = []
     for layout, k in (("standard", 1), ("standard", 8), ("standard", 16), ("band", 1), ("band", 8), ("band", 12)):
-        b = ShardedBoard(H, W, turns_per_launch=k, layout=layout)
-        assert b.use_band == (layout == "band")
-        b.load_random(1)
-        b.step(turns, count=True)
-        torch.cuda.synchronize()
-        fused = b.fused_count()
-        assert fused == b.alive_count()
-        hashes.append(b.hash())
-        del b
+        with golhip.Engine(H, W, device=0, layout=layout, turns_per_launch=k) as e:
+            assert e.info()["layout"] == layout and e.info()["turns_per_launch"] == k
+            e.load_random(1)
+            fused = e.step_counted(turns, turns).tolist()
+            assert fused == [e.alive_count()]
+            hashes.append(e.hash())
         torch.cuda.empty_cache()
     assert len(set(hashes)) == 1
 

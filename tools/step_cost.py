@@ -1,0 +1,70 @@
+"""Per-rank cost of the sharded step structure, measured on one GPU.
+
+    python tools/step_cost.py [--board weak|strong8|bit64k] [--steps 10]
+
+Each variant steps the same synthetic board (seed 1) with `steps` k-turn steps through the
+engine (gol_engine_step_counted, counts fused every k turns as bench.py does) and prints one
+JSON line: wall ms per step (host clock around the call) and the engine's step timing (HIP
+events: first launch of a shard-step to its last).  Variants:
+  local         one shard, the default step plan (edge rows || interior, exchange overlapped)
+  local-serial  one shard, exchange then one launch (GOL_STEP_SERIAL)
+  loopback1     one shard through the LOOPBACK transport (device copies of the plan)
+  loopback2     two shards on the same GPU (each half the rows, concurrent)
+  rccl1         one shard, RCCL send-to-self (the multi-GPU code path, one rank)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gol-distributed-final_amd")]
+
+BOARDS = {"weak": (1 << 17, 1 << 20), "strong8": (32768, 262144), "bit64k": (65536, 65536),
+          "strong262k": (262144, 262144)}
+VARIANTS = {
+    "local": dict(),
+    "local-serial": dict(serial_step=True),
+    "loopback1": dict(transport="loopback"),
+    "loopback2": dict(shards=2, same_device=True, transport="loopback"),
+    "rccl1": dict(transport="rccl"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--board", default="weak", choices=sorted(BOARDS))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+    import golhip
+    torch.cuda.set_device(0)
+    H, W = BOARDS[a.board]
+    ref = None
+    for rep in range(a.reps):
+        for name in a.variants.split(","):
+            with golhip.Engine(H, W, device=0, **VARIANTS[name]) as e:
+                k = e.info()["turns_per_launch"]
+                e.load_random(1)
+                e.step_counted(3 * k, k)
+                e.set_timing(True)
+                t0 = time.perf_counter()
+                counts = e.step_counted(a.steps * k, k)
+                dt = time.perf_counter() - t0
+                t = e.timing()
+                h = e.hash()
+            if ref is None:
+                ref = (h, counts.tolist())
+            line = {"board": a.board, "variant": name, "rep": rep, "k": k, "steps": a.steps,
+                    "wall_ms_per_step": round(dt / a.steps * 1e3, 4), "step_ms": round(t["mean_ms"], 4),
+                    "shard_steps": t["launches"], "TCUPS": round(H * W * k * a.steps / dt / 1e12, 2),
+                    "same_result": (h, counts.tolist()) == ref}
+            print(json.dumps(line), flush=True)
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
