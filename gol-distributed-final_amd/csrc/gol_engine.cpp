@@ -180,7 +180,7 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
     if (layout == GOL_LAYOUT_BAND && W % 1024 != 0) return gol_set_error(GOL_EINVAL, "the band layout needs W %% 1024 == 0");
     e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
     if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
-    e->step_flags = cfg ? (cfg->flags & GOL_STEP_SERIAL) : 0;
+    e->step_flags = cfg ? (cfg->flags & (GOL_STEP_SERIAL | GOL_STEP_EDGE_FIRST | GOL_STEP_OVERLAP)) : 0;
     return GOL_OK;
 }
 
@@ -565,6 +565,18 @@ static int timing_event(gol_engine *e, gol_shard &s, size_t *ev)
     return GOL_OK;
 }
 
+// The step plan of shard s (gol_step_plan flags): as configured, else OVERLAP when the shard's
+// launch runs many rounds of workgroups (the edge launches then share the CUs with the interior
+// at no cost: +1 % on the 2^17 x 2^20 board), SERIAL when it is a launch of one or a few rounds,
+// whose rank-weighted strips (gol_kernels.hip StripMap) assume they have the CUs to themselves
+// (a concurrent edge launch cost 7 % on a 32768 x 262144 shard, profiles/r03a_step_cost).
+static int step_mode(gol_engine *e, const gol_shard &s, int k)
+{
+    if (e->step_flags) return e->step_flags;
+    const double rounds = golk_step_rounds(e->band, s.R, e->Wd, k, e->band ? e->band_dw : e->dw, e->strip);
+    return rounds > GOL_OVERLAP_ROUNDS ? GOL_STEP_OVERLAP : GOL_STEP_SERIAL;
+}
+
 // k turns of every shard, as gol_step_plan lays them out: the edge rows (they read the halo)
 // on the edge stream and the interior beside them on the compute stream; the next step's halo
 // exchange starts as soon as the edge rows are written, while the interior is still running.
@@ -579,7 +591,7 @@ static int launch_k(gol_engine *e, int k, bool count)
         RCCHK(set_dev(s.device));
         gol_launch plan[3];
         int32_t np = 0;
-        RCCHK(gol_step_plan(s.R, k, e->kx, e->step_flags, plan, 3, &np));
+        RCCHK(gol_step_plan(s.R, k, e->kx, step_mode(e, s, k), plan, 3, &np));
         uint64_t *slots = count ? s.slots : nullptr;
         if (count) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
         size_t ev = 0;
@@ -589,6 +601,9 @@ static int launch_k(gol_engine *e, int k, bool count)
         }
         HIPCHK(hipEventRecord(s.ev_start, s.stream));  // the step's inputs are complete, slots zeroed
         bool edge_used = false, waited[2] = {false, false};
+        int last_halo = -1;  // the last launch that reads the halo writes the rows the exchange sends
+        for (int j = 0; j < np; ++j)
+            if (plan[j].needs_halo) last_halo = j;
         for (int j = 0; j < np; ++j) {
             const gol_launch &L = plan[j];
             const bool on_edge = L.stream == GOL_LAUNCH_EDGE;
@@ -602,13 +617,9 @@ static int launch_k(gol_engine *e, int k, bool count)
                 for (auto &t : e->sh) HIPCHK(hipStreamWaitEvent(st, t.ev_halo, 0));
             }
             RCCHK(step_launch(e, s, st, k, L.row0, L.rows, slots));
+            if (j == last_halo) HIPCHK(hipEventRecord(s.ev_edge, st));
         }
-        if (edge_used) {
-            HIPCHK(hipEventRecord(s.ev_edge, s.edge));
-            HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
-        } else {
-            HIPCHK(hipEventRecord(s.ev_edge, s.stream));
-        }
+        if (edge_used) HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
         if (e->timing) {
             HIPCHK(hipEventRecord(s.tev[ev + 1], s.stream));
             e->timed.push_back({i, ev, (double)s.R * (double)e->W * k});

@@ -15,6 +15,10 @@
 #define GOL_DEFAULT_BAND_K 12  // band layout, 4 words per lane: the split pipeline
 #define GOL_DEFAULT_DW 2       // standard layout: 64 cells per lane
 
+// A step whose launch runs more rounds of workgroups than this overlaps its edge launches with
+// the interior (GOL_STEP_OVERLAP), else it runs as one launch (gol_engine.cpp step_mode).
+#define GOL_OVERLAP_ROUNDS 4.0
+
 // Ghost rows kept above and below each bit buffer: the halo (received from the neighbouring
 // shards, or the torus wrap of a single shard) lands there, contiguous with the shard's rows,
 // so the kernels address input row y as board + y*pitch for -k <= y < R + k.

@@ -47,9 +47,15 @@ namespace golk {
 // v_bitop3_b32 truth tables: operand 0 -> 0xF0, operand 1 -> 0xCC, operand 2 -> 0xAA.
 constexpr unsigned TT_XOR3 = 0x96;  // a ^ b ^ c
 constexpr unsigned TT_MAJ = 0xE8;   // majority(a, b, c)
-constexpr unsigned TT_EQ1 = 0x14;   // (a ^ b) & ~c
-constexpr unsigned TT_EQ2 = 0x42;   // c ? ~(a | b) : (a & b)
-constexpr unsigned TT_MUX = 0xCA;   // a ? b : c
+// The rule tail (tools/rule_search.c, tests/test_rule_circuit_cpu.py): with T = t0 + 2(k0 + u +
+// 2v) the 3x3 sum including the cell, alive' = (T == 3) | (cell & T == 4)
+//   = (t0 | cell) & G2,  G2 = TT_G2(u, v, G1),  G1 = TT_G1(t0, k0, v)  (exactly one of t0, k0, v).
+// Three gates instead of the four of t0 ? [S == 1] : cell & [S == 2]: an exhaustive search over
+// 3-gate circuits finds them only when it may use that the centre row's horizontal sum includes
+// the cell (a centre sum of 0 means a dead cell, 3 a live one), which holds in every kernel here.
+constexpr unsigned TT_G1 = 0x16;    // exactly one of a, b, c
+constexpr unsigned TT_G2 = 0x29;    // (~a & ~b & ~c) | (~a & b & c) | (a & ~b & c)
+constexpr unsigned TT_OUT = 0xA8;   // (a | b) & c
 
 template <unsigned TT>
 __device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
@@ -124,8 +130,8 @@ __device__ __forceinline__ void store_words(uint32_t *p, const uint32_t (&w)[DW]
 }
 
 // B3/S23 from three horizontal sums (rows above/middle/below, value = h0 + 2*h1 in 0..3 per
-// cell) and the middle cell.  T = sum of the 3x3 block including the cell = t0 + 2*(k0 + u +
-// 2v); alive' = (T == 3) | (cell & T == 4).
+// cell; the middle one includes the cell) and the middle cell.  T = sum of the 3x3 block
+// including the cell = t0 + 2*(k0 + u + 2v); alive' = (T == 3) | (cell & T == 4): 7 gates.
 __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
                                          uint32_t c0, uint32_t c1, uint32_t cell)
 {
@@ -133,9 +139,9 @@ __device__ __forceinline__ uint32_t rule(uint32_t a0, uint32_t a1, uint32_t b0, 
     const uint32_t k0 = bitop3<TT_MAJ>(a0, b0, c0);
     const uint32_t u = bitop3<TT_XOR3>(a1, b1, c1);
     const uint32_t v = bitop3<TT_MAJ>(a1, b1, c1);
-    const uint32_t eq1 = bitop3<TT_EQ1>(u, k0, v);  // k0 + u + 2v == 1
-    const uint32_t eq2 = bitop3<TT_EQ2>(u, k0, v);  // k0 + u + 2v == 2
-    return bitop3<TT_MUX>(t0, eq1, eq2 & cell);
+    const uint32_t g1 = bitop3<TT_G1>(t0, k0, v);
+    const uint32_t g2 = bitop3<TT_G2>(u, v, g1);
+    return bitop3<TT_OUT>(t0, cell, g2);
 }
 
 // ------------------------------------------------------------------ register pipeline
@@ -222,10 +228,9 @@ __device__ __forceinline__ void sstage_wave3(Pipe<K, 1> &p, uint32_t (&c)[3])
     GOL_ROWS3(u[r] = bitop3<TT_XOR3>(p.h1[g[r]][A][0], p.h1[g[r]][M][0], p.h1[g[r]][r][0]))
     GOL_ROWS3(v[r] = bitop3<TT_MAJ>(p.h1[g[r]][A][0], p.h1[g[r]][M][0], p.h1[g[r]][r][0]))
     GOL_ROWS3(t0[r] = bitop3<TT_XOR3>(p.h0[g[r]][A][0], p.h0[g[r]][M][0], p.h0[g[r]][r][0]))
-    GOL_ROWS3(e2[r] = bitop3<TT_EQ2>(u[r], k0[r], v[r]))
-    GOL_ROWS3(e1[r] = bitop3<TT_EQ1>(u[r], k0[r], v[r]))
-    GOL_ROWS3(e2[r] &= p.cc[g[r]][M][0])
-    GOL_ROWS3(c[r] = bitop3<TT_MUX>(t0[r], e1[r], e2[r]))
+    GOL_ROWS3(e1[r] = bitop3<TT_G1>(t0[r], k0[r], v[r]))
+    GOL_ROWS3(e2[r] = bitop3<TT_G2>(u[r], v[r], e1[r]))
+    GOL_ROWS3(c[r] = bitop3<TT_OUT>(t0[r], p.cc[g[r]][M][0], e2[r]))
 #undef GOL_ROWS3
 }
 // All NSTG stages of one 3-row block (steps 0 .. NSTG + 1).
@@ -471,13 +476,11 @@ __device__ __forceinline__ void bstage(Pipe<K, DW> &p, const int g, uint32_t (&c
 #pragma unroll
     for (int j = 0; j < DW; ++j) t0[j] = bitop3<TT_XOR3>(a0[j], b0[j], c0[j]);
 #pragma unroll
-    for (int j = 0; j < DW; ++j) e2[j] = bitop3<TT_EQ2>(u[j], k0[j], v[j]);
+    for (int j = 0; j < DW; ++j) e1[j] = bitop3<TT_G1>(t0[j], k0[j], v[j]);
 #pragma unroll
-    for (int j = 0; j < DW; ++j) e1[j] = bitop3<TT_EQ1>(u[j], k0[j], v[j]);
+    for (int j = 0; j < DW; ++j) e2[j] = bitop3<TT_G2>(u[j], v[j], e1[j]);
 #pragma unroll
-    for (int j = 0; j < DW; ++j) e2[j] &= p.cc[g][SM][j];
-#pragma unroll
-    for (int j = 0; j < DW; ++j) cur[j] = bitop3<TT_MUX>(t0[j], e1[j], e2[j]);
+    for (int j = 0; j < DW; ++j) cur[j] = bitop3<TT_OUT>(t0[j], p.cc[g][SM][j], e2[j]);
 }
 
 // Same stage with the rule evaluated word by word (fewer live temporaries than bstage; at
@@ -2281,6 +2284,16 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
 }
 
 int golk_band_useful_words(int k, int dw) { return band_useful_words(k, dw); }
+
+double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int strip)
+{
+    if (!band || dw != 4 || k != 12 || rows <= 0) return 1e9;
+    const int64_t ngroups = (Wd + band_useful_words(k, dw) - 1) / band_useful_words(k, dw);
+    const int64_t slots = resident_workgroups((const void *)band_pipe_kernel<3, 4, true, true>, 256);
+    if (slots <= 0) return 1e9;
+    const int64_t st = strip > 0 ? strip : 1024;  // launch_band_pipe's strips: up to 1024 rows
+    return (double)(ngroups * ((rows + st - 1) / st)) / (double)slots;
+}
 
 hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
                              int64_t spitch, int64_t dpitch, hipStream_t s)

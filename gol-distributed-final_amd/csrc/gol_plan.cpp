@@ -47,15 +47,18 @@ extern "C" int gol_step_plan(int64_t R, int32_t k, int32_t kx, int32_t flags, go
         return gol_set_error(GOL_EINVAL, "bad step plan arguments (R %lld, k %d, kx %d)", (long long)R, k, kx);
     gol_launch plan[3];
     int m = 0;
-    if ((flags & GOL_STEP_SERIAL) || R < 3 * (int64_t)kx) {
+    const bool split = !(flags & GOL_STEP_SERIAL) && (flags & (GOL_STEP_OVERLAP | GOL_STEP_EDGE_FIRST)) &&
+                       R >= 3 * (int64_t)kx;
+    if (!split) {
         // one launch over every row, once the halo is in; the next exchange waits for it
         plan[m++] = {GOL_LAUNCH_MAIN, 1, 0, R};
     } else {
-        // the rows the next exchange sends (and that need this step's halo) first, on the edge
-        // stream; the interior [kx, R - kx) reads no ghost row and runs beside them and beside
-        // the next exchange
-        plan[m++] = {GOL_LAUNCH_EDGE, 1, 0, kx};
-        plan[m++] = {GOL_LAUNCH_EDGE, 1, R - kx, kx};
+        // the rows the next exchange sends (and that need this step's halo) first -- on the edge
+        // stream (OVERLAP) or ahead of the interior on the compute stream (EDGE_FIRST); the
+        // interior [kx, R - kx) reads no ghost row and runs beside the next exchange
+        const int32_t st = (flags & GOL_STEP_OVERLAP) ? GOL_LAUNCH_EDGE : GOL_LAUNCH_MAIN;
+        plan[m++] = {st, 1, 0, kx};
+        plan[m++] = {st, 1, R - kx, kx};
         plan[m++] = {GOL_LAUNCH_MAIN, 0, kx, R - 2 * (int64_t)kx};
     }
     for (int i = 0; i < m && i < cap; ++i) out[i] = plan[i];

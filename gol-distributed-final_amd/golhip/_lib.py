@@ -29,7 +29,8 @@ GOL_TRANSPORT_AUTO, GOL_TRANSPORT_LOOPBACK, GOL_TRANSPORT_RCCL, GOL_TRANSPORT_LO
 TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "rccl": GOL_TRANSPORT_RCCL}
 TRANSPORT_NAMES = {GOL_TRANSPORT_LOOPBACK: "loopback", GOL_TRANSPORT_RCCL: "rccl", GOL_TRANSPORT_LOCAL: "local"}
 GOL_SHARDS_SAME_DEVICE = 1
-GOL_STEP_SERIAL = 2
+GOL_STEP_SERIAL, GOL_STEP_EDGE_FIRST, GOL_STEP_OVERLAP = 2, 4, 8
+STEP_MODES = {"auto": 0, "serial": GOL_STEP_SERIAL, "edge_first": GOL_STEP_EDGE_FIRST, "overlap": GOL_STEP_OVERLAP}
 GOL_HALO_SEND, GOL_HALO_RECV = 0, 1
 GOL_LAUNCH_MAIN, GOL_LAUNCH_EDGE = 0, 1
 
@@ -161,14 +162,17 @@ def _one_hip_runtime():
         pass
 
 
-def load(path: str):
-    """Bind the C ABI of the shared object at `path` (raises if it is missing)."""
+def load(path: str, strict: bool = True):
+    """Bind the C ABI of the shared object at `path` (raises if it is missing).  strict=False
+    (same-box A/B builds of older revisions, tools/ab.py) skips entry points it lacks."""
     _one_hip_runtime()
     if not os.path.exists(path):
         raise GolError(GOL_ESTATE, f"{path} is missing: run __graft_entry__.build() "
                                    "(hipcc --offload-arch=gfx950); there is no CPU fallback")
     L = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
+        if not strict and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -197,12 +201,13 @@ def halo_plan(H: int, nranks: int, rank: int, k: int) -> list[tuple[str, int, in
     return [("send" if o.kind == GOL_HALO_SEND else "recv", o.peer, o.row, o.rows) for o in ops[:n.value]]
 
 
-def step_plan(R: int, k: int, kx: int, serial: bool = False) -> list[tuple[str, bool, int, int]]:
-    """gol_step_plan: the launches of one k-turn step of an R-row shard, as (stream "main"/"edge",
-    needs_halo, first output row, rows)."""
+def step_plan(R: int, k: int, kx: int, mode: str = "overlap") -> list[tuple[str, bool, int, int]]:
+    """gol_step_plan: the launches of one k-turn step of an R-row shard in launch order, as
+    (stream "main"/"edge", needs_halo, first output row, rows); mode "overlap", "edge_first" or
+    "serial"."""
     out = (gol_launch * 3)()
     n = ctypes.c_int32()
-    check(lib().gol_step_plan(R, k, kx, GOL_STEP_SERIAL if serial else 0, out, 3, ctypes.byref(n)))
+    check(lib().gol_step_plan(R, k, kx, STEP_MODES[mode], out, 3, ctypes.byref(n)))
     return [("edge" if L.stream == GOL_LAUNCH_EDGE else "main", bool(L.needs_halo), L.row0, L.rows)
             for L in out[:n.value]]
 

@@ -14,8 +14,8 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (GOL_RCCL_ID_BYTES, GOL_WRITE_FN, GOL_SHARDS_SAME_DEVICE, GOL_STEP_SERIAL, LAYOUTS, TRANSPORT_NAMES, TRANSPORTS,
-                   GolError, check, gol_config, lib)
+from ._lib import (GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_WRITE_FN, LAYOUTS, STEP_MODES, TRANSPORT_NAMES,
+                   TRANSPORTS, GolError, check, gol_config, lib)
 
 
 def rccl_unique_id(library=None) -> bytes:
@@ -31,14 +31,14 @@ def rccl_unique_id(library=None) -> bytes:
 class Engine:
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
                  strip_rows: int = 0, device: int = -1, layout: str = "auto", shards: int = 1,
-                 transport: str = "auto", same_device: bool = False, serial_step: bool = False, library=None,
+                 transport: str = "auto", same_device: bool = False, step: str = "auto", library=None,
                  _rank=None):
         self.H, self.W = int(height), int(width)
         self._L = library or lib()
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, strip_rows=strip_rows,
                          cells_per_lane=cells_per_lane, layout=LAYOUTS[layout], shards=shards,
                          transport=TRANSPORTS[transport],
-                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | (GOL_STEP_SERIAL if serial_step else 0))
+                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | STEP_MODES[step])
         h = ctypes.c_void_p()
         if _rank is None:
             self._check(self._L.gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))

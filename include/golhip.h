@@ -114,6 +114,8 @@ typedef struct gol_engine gol_engine;
 /* gol_config.flags */
 #define GOL_SHARDS_SAME_DEVICE 1 /* every local shard on `device` (loopback testing on one GPU) */
 #define GOL_STEP_SERIAL 2        /* one launch per shard and step, after the halo exchange (gol_step_plan) */
+#define GOL_STEP_EDGE_FIRST 4    /* the edge rows first on the compute stream, then the interior (gol_step_plan) */
+#define GOL_STEP_OVERLAP 8       /* the edge rows on the edge stream beside the interior (gol_step_plan) */
 typedef struct gol_config {
     int32_t device;           /* HIP device ordinal (first shard); -1 = current device */
     int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
@@ -248,13 +250,21 @@ typedef struct gol_halo_op {
 } gol_halo_op;
 int gol_halo_plan(int64_t H, int32_t nranks, int32_t rank, int32_t k, gol_halo_op *ops, int32_t cap, int32_t *n);
 /* gol_step_plan: the launches of one k-turn step of a shard of R rows whose
- * halo exchanges carry kx >= k rows.  EDGE launches run on the shard's edge
- * stream once the halo is in; MAIN launches on its compute stream.  With
- * R >= 3 kx (and no GOL_STEP_SERIAL): rows [0, kx) and [R - kx, R) on the edge
- * stream, the interior [kx, R - kx) (it reads no ghost row) on the compute
- * stream beside them, and the next step's exchange starts when the edge rows
- * are written.  Otherwise one MAIN launch over [0, R) after the halo.  Writes
- * min(n, cap) launches. */
+ * halo exchanges carry kx >= k rows, in launch order.  EDGE launches run on
+ * the shard's edge stream, MAIN launches on its compute stream; a launch that
+ * needs_halo waits for the exchange.  The next step's exchange starts when the
+ * last launch that needs the halo (they write rows [0, kx) and [R - kx, R),
+ * the rows it sends) is done.  With R >= 3 kx:
+ *  - GOL_STEP_OVERLAP: rows [0, kx) and [R - kx, R) on the edge stream, the
+ *    interior [kx, R - kx) (it reads no ghost row) on the compute stream
+ *    beside them: nothing waits for the exchange but the edge launches;
+ *  - GOL_STEP_EDGE_FIRST: the same three launches in order on the compute
+ *    stream (the exchange overlaps the interior; no second kernel competes
+ *    with the interior for the CUs);
+ *  - neither (or GOL_STEP_SERIAL, or R < 3 kx): one MAIN launch over [0, R).
+ * The engine picks per step: OVERLAP for launches of many
+ * rounds of workgroups, SERIAL below, unless gol_config.flags forces one.
+ * Writes min(n, cap) launches. */
 #define GOL_LAUNCH_MAIN 0
 #define GOL_LAUNCH_EDGE 1
 typedef struct gol_launch {

@@ -319,10 +319,10 @@ def test_timing_counts_the_step_launches(G):
     with _sharded(G, 600, 2048, 2) as e:
         e.load_random(1)
         e.set_timing(True)
-        e.step(36)  # 3 launches of k = 12, each with an interior launch per shard
+        e.step(36)  # 3 steps of k = 12 on each of the 2 shards, every launch of a step inside its timing
         t = e.timing()
         assert t["launches"] == 6 and t["mean_ms"] > 0
-        assert t["mean_cell_updates"] == (300 - 24) * 2048 * 12
+        assert t["mean_cell_updates"] == 300 * 2048 * 12
 
 
 def test_device_fault_is_reported(G):

@@ -78,26 +78,29 @@ def test_halo_plan_errors(G):
             G.halo_plan(*args)
 
 
-@pytest.mark.parametrize("R,k,kx,serial", [(1000, 12, 12, False), (1000, 1, 12, False), (36, 12, 12, False),
-                                           (35, 12, 12, False), (13, 8, 12, False), (1000, 12, 12, True),
-                                           (5, 1, 1, False), (3, 1, 1, False), (2, 1, 1, False)])
-def test_step_plan_covers_rows_once(G, R, k, kx, serial):
+@pytest.mark.parametrize("mode", ["overlap", "edge_first", "serial"])
+@pytest.mark.parametrize("R,k,kx", [(1000, 12, 12), (1000, 1, 12), (36, 12, 12), (35, 12, 12), (13, 8, 12),
+                                    (5, 1, 1), (3, 1, 1), (2, 1, 1)])
+def test_step_plan_covers_rows_once(G, R, k, kx, mode):
     if kx > R:
         pytest.skip("kx > R")
-    plan = G.step_plan(R, k, kx, serial)
+    plan = G.step_plan(R, k, kx, mode)
+    split = mode != "serial" and R >= 3 * kx
     cover = np.zeros(R, dtype=int)
     for stream, needs_halo, row0, rows in plan:
         cover[row0:row0 + rows] += 1
         reads_ghosts = row0 - k < 0 or row0 + rows + k > R
         assert needs_halo == reads_ghosts, (stream, row0, rows)
-        assert stream == "edge" or not needs_halo or len(plan) == 1
+        assert (stream == "edge") == (split and mode == "overlap" and needs_halo)
     assert (cover == 1).all()
-    if not serial and R >= 3 * kx:
-        # the rows the next exchange sends are written by the edge launches alone
-        edge = np.zeros(R, dtype=bool)
-        for stream, _, row0, rows in plan:
-            if stream == "edge":
-                edge[row0:row0 + rows] = True
-        assert edge[:kx].all() and edge[R - kx:].all() and not edge[kx:R - kx].any()
+    if split:
+        # the rows the next exchange sends are written by the launches that read the halo, all
+        # of them before the interior in launch order
+        halo = np.zeros(R, dtype=bool)
+        for stream, needs_halo, row0, rows in plan:
+            if needs_halo:
+                halo[row0:row0 + rows] = True
+        assert halo[:kx].all() and halo[R - kx:].all() and not halo[kx:R - kx].any()
+        assert [h for _, h, _, _ in plan] == [True, True, False]
     else:
         assert plan == [("main", True, 0, R)]

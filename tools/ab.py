@@ -19,7 +19,7 @@ import sys, json
 sys.path[:0] = [%r, %r]
 import golhip._lib as L
 if %r != "lib":
-    L._lib = L.load(%r)
+    L._lib = L.load(%r, strict=False)
 sys.argv = ["bench.py"] + %r
 import bench
 bench.main()

@@ -6,7 +6,9 @@ Each variant steps the same synthetic board (seed 1) with `steps` k-turn steps t
 engine (gol_engine_step_counted, counts fused every k turns as bench.py does) and prints one
 JSON line: wall ms per step (host clock around the call) and the engine's step timing (HIP
 events: first launch of a shard-step to its last).  Variants:
-  local         one shard, the default step plan (edge rows || interior, exchange overlapped)
+  local         one shard, the engine's choice of step plan (overlap for many-round launches)
+  local-overlap one shard, edge rows on the edge stream beside the interior (GOL_STEP_OVERLAP)
+  local-edgefirst  edge rows, then the interior, on one stream (GOL_STEP_EDGE_FIRST)
   local-serial  one shard, exchange then one launch (GOL_STEP_SERIAL)
   loopback1     one shard through the LOOPBACK transport (device copies of the plan)
   loopback2     two shards on the same GPU (each half the rows, concurrent)
@@ -25,7 +27,9 @@ BOARDS = {"weak": (1 << 17, 1 << 20), "strong8": (32768, 262144), "bit64k": (655
           "strong262k": (262144, 262144)}
 VARIANTS = {
     "local": dict(),
-    "local-serial": dict(serial_step=True),
+    "local-overlap": dict(step="overlap"),
+    "local-edgefirst": dict(step="edge_first"),
+    "local-serial": dict(step="serial"),
     "loopback1": dict(transport="loopback"),
     "loopback2": dict(shards=2, same_device=True, transport="loopback"),
     "rccl1": dict(transport="rccl"),
