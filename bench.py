@@ -70,6 +70,7 @@ def parse(argv=None):
                          "and max-over-ranks timing on a 1-GPU box")
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration only (no GPU): ranks, barriers and the JSON line, value 0")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank exits at once
     return ap.parse_args(argv)
 
 
@@ -82,21 +83,42 @@ def _free_port() -> int:
     return port
 
 
-def self_launch(args) -> int:
+def self_launch(args, timeout_s: float = 900.0) -> int:
     """Start the N ranks as child processes (this process never touches the GPU) and print
-    rank 0's JSON line; nonzero exit if any rank fails."""
+    rank 0's JSON line.  Every rank is waited for (bounded by timeout_s); when one fails or the
+    time is up, the survivors -- blocked in a collective with the dead rank -- are terminated,
+    then killed, and the exit status is nonzero."""
+    import tempfile
     port = _free_port()
     procs = []
+    out0 = tempfile.TemporaryFile()
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].communicate()[0].decode(errors="replace")
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    deadline = time.monotonic() + timeout_s
     rc = 0
-    for p in procs:
-        rc = rc or p.wait()
-    sys.stdout.write(out)
+    while True:
+        codes = [p.poll() for p in procs]
+        failed = [c for c in codes if c not in (None, 0)]
+        if failed or all(c == 0 for c in codes) or time.monotonic() > deadline:
+            rc = failed[0] if failed else (0 if all(c == 0 for c in codes) else 124)
+            break
+        time.sleep(0.2)
+    if rc:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        end = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out0.seek(0)
+    sys.stdout.write(out0.read().decode(errors="replace"))
     sys.stdout.flush()
     return rc
 
@@ -391,6 +413,8 @@ def main():
         sys.exit(self_launch(args))
     if args.k <= 0 and args.workload == "byte16k":
         args.k = 32  # pipelined byte kernel, 8 waves x 4 turns
+    if int(os.environ.get("RANK", "0")) == args.fail_rank:
+        sys.exit(3)  # (tests/test_bench_cpu.py: the other ranks wait in a collective for it)
     ranks = Ranks(args)
     if args.dry_run:
         ranks.barrier()

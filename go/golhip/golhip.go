@@ -113,6 +113,9 @@ func NewBroker(cfg Config) (*Broker, error) {
 // Close releases the GPU state.
 func (s *Broker) Close() { C.gol_broker_destroy(s.b) }
 
+// aliveBufPairs bounds the alive-list buffer handed to C per call (pairs of int32).
+const aliveBufPairs = 1 << 20
+
 type brokerCall func(*C.gol_broker, *C.gol_request, *C.gol_response) C.int
 
 // call runs one broker method with Go-owned buffers, borrowed by C for the call only.  The
@@ -142,10 +145,17 @@ func (s *Broker) call(f brokerCall, req Request, res *Response, wantWorld bool) 
 		cres.World = bytePtr(world)
 		cres.world_stride = C.int64_t(w)
 	}
-	alive := make([]C.int32_t, 2*h*w+2)
+	// The alive list (broker.go:47-58) comes back through a bounded buffer: a typical board's
+	// list fits; a longer one is rebuilt here from the returned World (the same rule: every
+	// byte != 0, row-major) instead of reserving 8 bytes per cell on every call.
+	capPairs := h * w
+	if capPairs > aliveBufPairs {
+		capPairs = aliveBufPairs
+	}
+	alive := make([]C.int32_t, 2*capPairs+2)
 	pin.Pin(&alive[0])
 	cres.Alive = &alive[0]
-	cres.alive_cap = C.int64_t(h * w)
+	cres.alive_cap = C.int64_t(capPairs)
 	if err := check(f(s.b, &creq, &cres)); err != nil {
 		return err
 	}
@@ -153,9 +163,21 @@ func (s *Broker) call(f brokerCall, req Request, res *Response, wantWorld bool) 
 	if world != nil {
 		res.World = rows(world, h, w)
 	}
-	res.Alive = make([]Cell, int(cres.alive_len))
-	for i := range res.Alive {
-		res.Alive[i] = Cell{X: int(alive[2*i]), Y: int(alive[2*i+1])}
+	n := int(cres.alive_len)
+	if n <= capPairs {
+		res.Alive = make([]Cell, n)
+		for i := range res.Alive {
+			res.Alive[i] = Cell{X: int(alive[2*i]), Y: int(alive[2*i+1])}
+		}
+	} else {
+		res.Alive = make([]Cell, 0, n)
+		for y := 0; y < h; y++ {
+			for x, v := range world[y*w : (y+1)*w] {
+				if v != 0 {
+					res.Alive = append(res.Alive, Cell{X: x, Y: y})
+				}
+			}
+		}
 	}
 	return nil
 }

@@ -28,6 +28,19 @@ def test_self_launch_two_ranks_dry_run():
         assert key in d
 
 
+def test_self_launch_ends_when_a_rank_dies():
+    """A rank that dies leaves its peers blocked in a collective with it: the launcher must not
+    wait for them forever -- it terminates the survivors and returns the failure."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--dry-run", "--fail-rank", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert time.monotonic() - t0 < 60
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_world_size_mismatch_is_an_error():
     env = dict(os.environ, WORLD_SIZE="3", RANK="0")
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run"], cwd=ROOT, env=env,
