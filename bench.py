@@ -223,7 +223,13 @@ def roofline(kind, launch_ms, cell_updates, pmc, pmc_note):
     if valu:
         ach = valu / sec / 1e9
         r.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
-                  "unit": "G wave64 VALU inst/s", "frac": round(ach / VALU_PEAK_GINST, 4)})
+                  "unit": "G wave64 VALU inst/s", "frac": round(ach / VALU_PEAK_GINST, 4),
+                  # the same kernel at the shader clock its profile measured (the chip lowers its
+                  # clock under this load: power), and its work per instruction
+                  "profile_clock_GHz": pmc.get("clock_GHz"),
+                  "frac_at_profile_clock": round(ach / (VALU_PEAK_GINST / 2.4 * pmc["clock_GHz"]), 4)
+                  if pmc.get("clock_GHz") else None,
+                  "cell_updates_per_valu_lane_op": round(cell_updates / (valu * 64), 3)})
     else:  # no PMC profile of this kernel build: only the HBM side can be stated (None without traffic)
         r.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": hbm["frac"]})

@@ -12,6 +12,9 @@
 
 // Per-device error word for launches made without one (lazily allocated, zeroed).
 uint32_t *golk_device_err_word(int device);
+// Per-device CU slot masks of the band pipeline's role placement (indexed by XCC, SE, SH, CU).
+#define GOL_CU_SLOT_WORDS 2048
+uint32_t *golk_cu_slots(int device);
 // Paired-rank claim counters (one buffer per launch stream, gol_kernels.hip StripMap).
 // golk_reset_claims: zero the buffer of stream s, ordered on s (after a faulted launch).
 // golk_release_claims: free it (the caller has synchronised s; an engine destroying its streams).

@@ -272,6 +272,7 @@ struct BitsArgs {
     int32_t strip, ngroups;
     uint64_t *slots;
     uint32_t *err;
+    uint32_t *cu_slots;  // band pipeline: per-CU masks of the workgroup slots in use (GOL_CU_SLOT_WORDS)
     StripMap sm;
 };
 
@@ -704,6 +705,43 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 // ROWF: hand-off flags count rows instead of 3-row blocks, so a reader may read a row as soon as
 // it is written (one-round launches: +1.2 % on 65536^2; the weak board measured -0.4 % and keeps
 // block flags).
+// Role placement (GOL_BAND_PLACE): a workgroup of the band pipeline claims a free slot q (0..3) in
+// its CU's mask and each wave takes pipeline role (its SIMD + q) % 4, so that the (up to) four
+// workgroups resident on a CU put one wave of every role on every SIMD.  (Roles by wave index +
+// a per-workgroup rotation put two waves of one role on a SIMD for 64-75 % of the waves,
+// tools/timeline.py, profiles/r03/r03h_tl_roles.jsonl.)  Vector atomics of lane 0.
+#ifndef GOL_BAND_PLACE
+#define GOL_BAND_PLACE 1
+#endif
+__device__ __forceinline__ uint32_t cu_slot_index()
+{
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // XCC_ID
+    return (xcc << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 0xFu);
+}
+__device__ __forceinline__ int claim_cu_slot(uint32_t *m)
+{
+    uint32_t cur = __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t fr = ~cur & 0xFu;
+        if (!fr) return -1;
+        const int b = __ffs(fr) - 1;
+        const uint32_t old = atomicCAS(m, cur, cur | (1u << b));
+        if (old == cur) return b;
+        cur = old;
+    }
+    return -1;
+}
+
+// Cache policy bits of the band pipeline's output stores (2 = nt, streaming).
+#ifndef GOL_BAND_STORE_AUX
+#define GOL_BAND_STORE_AUX 2
+#endif
+// Pipeline shape of k = 12 (measurement builds may change it): KW stages in each of P waves.
+#ifndef GOL_BAND_KW
+#define GOL_BAND_KW 3
+#define GOL_BAND_P 4
+#endif
 template <int KW, int P, bool CONTIG, bool COUNT, int NPIPE = 1, bool ROWF = false>
 __global__ void __launch_bounds__(64 * P * NPIPE)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
@@ -714,12 +752,13 @@ band_pipe_kernel(BitsArgs a)
     constexpr int HL = band_halo_lanes(K, DW);
     constexpr int U = band_useful_words(K, DW);
     constexpr int ROW = 64 * DW;
-    constexpr int NS = 3;
+    constexpr int NS = 3;  // (the loops below are unrolled over the 3 slots)
     __shared__ uint32_t in_ring_[NPIPE][NS][3][ROW];
     __shared__ uint32_t ring_[NPIPE][P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
     __shared__ int ready_[NPIPE][P], consumed_[NPIPE][P];
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (never read; all waves share it)
     __shared__ int simd_of[NPIPE > 1 ? NPIPE * P : 1];
+    __shared__ int place_[P + 2];  // GOL_BAND_PLACE: SIMD of each wave, the CU slot, the mask index
 
     const int lane = threadIdx.x & 63;
     int pipe = 0, stage = 0;
@@ -746,8 +785,9 @@ band_pipe_kernel(BitsArgs a)
     // Pipeline position of this wave, rotated per workgroup: the waves of a workgroup sit on the
     // CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put its
     // loader (global_load_lds) on one SIMD and its storer on another.
-    const int wv = NPIPE > 1 ? stage : __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
+    int wv = NPIPE > 1 ? stage : __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
     uint32_t (*const in_ring)[3][ROW] = in_ring_[pipe];
+    constexpr bool PLACE = GOL_BAND_PLACE && NPIPE == 1 && P == 4;
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
     const int64_t band_q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
@@ -789,8 +829,21 @@ band_pipe_kernel(BitsArgs a)
 
     if (NPIPE == 1 && !has_rows) return;  // whole workgroup (no barrier after this point)
     if (threadIdx.x < NPIPE * P) { ready_[threadIdx.x / P][threadIdx.x % P] = 0; consumed_[threadIdx.x / P][threadIdx.x % P] = 0; }
+    if constexpr (PLACE) {
+        if (lane == 0) place_[threadIdx.x >> 6] = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u);
+        if (threadIdx.x == 0) {
+            const uint32_t idx = cu_slot_index();
+            place_[P] = a.cu_slots ? claim_cu_slot(a.cu_slots + idx) : -1;
+            place_[P + 1] = (int)idx;
+        }
+    }
     __syncthreads();
     if (!has_rows) return;  // a pipeline without rows (no barrier after this point)
+    if constexpr (PLACE) {
+        const int q = place_[P];
+        const int m = (1 << place_[0]) | (1 << place_[1]) | (1 << place_[2]) | (1 << place_[3]);
+        if (q >= 0 && m == 0xF) wv = __builtin_amdgcn_readfirstlane((place_[threadIdx.x >> 6] + q) & 3);
+    }
     lds_u32 *const ring_l = (lds_u32 *)&ring_[pipe][0][0][0][0];
     lds_u32 *const in_l = (lds_u32 *)&in_ring_[pipe][0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready_[pipe][0];
@@ -852,7 +905,9 @@ band_pipe_kernel(BitsArgs a)
     uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch_b;
     const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch_b;
     auto emit = [&](const uint32_t (&cur)[DW]) {
-        __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, 2);
+#ifndef GOL_EXP_NOSTORE  // (measurement builds only: -DGOL_EXP_NOSTORE drops the stores)
+        __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, GOL_BAND_STORE_AUX);
+#endif
         // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are masked
         // once at the end)
         if constexpr (COUNT) {
@@ -1010,6 +1065,9 @@ band_pipe_kernel(BitsArgs a)
     alive &= st_mask;  // halo lanes' rows are not this group's
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (COUNT && wv == P - 1) slot_add(a.slots, alive);
+    if constexpr (PLACE) {  // the last wave of the pipeline frees the workgroup's CU slot
+        if (wv == P - 1 && lane == 0 && place_[P] >= 0) atomicAnd(a.cu_slots + place_[P + 1], ~(1u << place_[P]));
+    }
 }
 
 // 32 x 32 bit-matrix transpose in registers: afterwards x[i] bit b = (before) x[b] bit i.
@@ -1879,6 +1937,26 @@ uint32_t *golk_device_err_word(int device)
     return w;
 }
 
+// Per-device CU slot masks of the band pipeline (GOL_BAND_PLACE; zeroed once, every workgroup
+// frees its slot on exit).
+uint32_t *golk_cu_slots(int device)
+{
+    static std::mutex mu;
+    static std::map<int, uint32_t *> tabs;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = tabs.find(device);
+    if (it != tabs.end()) return it->second;
+    int prev = 0;
+    uint32_t *w = nullptr;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return nullptr;
+    if (hipMalloc(&w, GOL_CU_SLOT_WORDS * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(w, 0, GOL_CU_SLOT_WORDS * sizeof(uint32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        w = nullptr;
+    (void)hipSetDevice(prev);
+    if (w) tabs[device] = w;
+    return w;
+}
+
 static uint32_t *err_or_default(uint32_t *err)
 {
     if (err) return err;
@@ -1972,6 +2050,7 @@ hipError_t golk_bits_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.slots = slots;
     a.sm = StripMap{};
     a.err = nullptr;  // no flag waits in this kernel
+    a.cu_slots = nullptr;
     if (rows <= 0) return hipSuccess;
     switch (dw) {
     case 1: return launch_bits_k<1>(k, a, s);
@@ -2193,7 +2272,7 @@ static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
-    constexpr int KW = 3, P = 4;
+    constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
     if constexpr (GOL_BAND_NPIPE > 1) {  // measurement build: pipelines on one SIMD each
         constexpr int NP = GOL_BAND_NPIPE;
         const bool count = a.slots != nullptr;
@@ -2265,6 +2344,11 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.sm = StripMap{};
     a.err = err_or_default(err);
     if (!a.err) return hipErrorOutOfMemory;
+    a.cu_slots = nullptr;
+    if (GOL_BAND_PLACE) {
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) a.cu_slots = golk_cu_slots(dev);
+    }
     const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
     const int U = band_useful_words(k, dw);
     a.ngroups = (int)((Wd + U - 1) / U);
@@ -2289,7 +2373,7 @@ double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int 
 {
     if (!band || dw != 4 || k != 12 || rows <= 0) return 1e9;
     const int64_t ngroups = (Wd + band_useful_words(k, dw) - 1) / band_useful_words(k, dw);
-    const int64_t slots = resident_workgroups((const void *)band_pipe_kernel<3, 4, true, true>, 256);
+    const int64_t slots = resident_workgroups((const void *)band_pipe_kernel<GOL_BAND_KW, GOL_BAND_P, true, true>, 64 * GOL_BAND_P);
     if (slots <= 0) return 1e9;
     const int64_t st = strip > 0 ? strip : 1024;  // launch_band_pipe's strips: up to 1024 rows
     return (double)(ngroups * ((rows + st - 1) / st)) / (double)slots;

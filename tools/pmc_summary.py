@@ -31,11 +31,19 @@ for d in sorted(os.listdir(src)):
         continue
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        acc[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        # one kernel can be launched with several grids (a step's interior and its edge rows):
+        # dispatches are grouped by (kernel, grid size)
+        acc[(f'{r["Kernel_Name"]} @grid {r["Grid_Size"]}', r["Counter_Name"])].append(float(r["Counter_Value"]))
     for (k, c), v in acc.items():
         means[k][c] = sum(v) / len(v)
 
-stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
+# mean duration per (kernel, grid) from the trace pass
+durs = collections.defaultdict(list)
+for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+    g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+    durs[f'{r["Kernel_Name"]} @grid {g}'].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+stats = {k: {"AverageNs": sum(v) / len(v), "Calls": len(v), "TotalNs": sum(v)} for k, v in durs.items()}
+json.dump(stats, open(os.path.join(dst, "kernel_grid_stats.json"), "w"), indent=1)
 out = {}
 for k, c in means.items():
     ns = float(stats[k]["AverageNs"]) if k in stats else None
@@ -54,13 +62,13 @@ for k, c in means.items():
 json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 if not out:
     sys.exit(f"no PMC counter rows under {src}")
-main = max(out, key=lambda k: out[k].get("avg_ns_trace") or 0)
+main = max(out, key=lambda k: stats.get(k, {}).get("TotalNs", 0))
 tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 t = json.load(open(tp)) if os.path.exists(tp) else {}
 src_hash = hashlib.sha256(open(os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernels.hip"),
                                 "rb").read()).hexdigest()[:16]
 if "hbm_bytes_per_launch" in out[main]:
-    t[key] = {"kernel": main, "kernel_src": src_hash, "bytes_per_launch": out[main]["hbm_bytes_per_launch"],
+    t[key] = {"kernel": main, "kernel_src": src_hash, "trace_calls": stats[main]["Calls"], "bytes_per_launch": out[main]["hbm_bytes_per_launch"],
               "profile": f"profiles/{tag}", "avg_ns_trace": out[main]["avg_ns_trace"]}
     c = out[main]["counters"]
     if "SQ_INSTS_VALU" in c:

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--nocount", action="store_true", help="plain steps (no fused alive count)")
+    ap.add_argument("--zero", action="store_true", help="an all-dead board (same instructions, no bit toggling)")
     a = ap.parse_args()
     import torch
     import golhip
@@ -53,16 +55,27 @@ def main():
             with golhip.Engine(H, W, device=0, **VARIANTS[name]) as e:
                 k = e.info()["turns_per_launch"]
                 e.load_random(1)
+                if a.zero:  # clear shard 0's bits in place (one shard): hipMemset from torch's HIP runtime
+                    import ctypes
+                    ptr, pitch = e.device_bits()
+                    hip = ctypes.CDLL("libamdhip64.so")
+                    assert hip.hipMemset(ctypes.c_void_p(ptr), 0, ctypes.c_size_t(H * pitch * 4)) == 0
+                    assert hip.hipDeviceSynchronize() == 0
+                    assert e.alive_count() == 0
                 e.step_counted(3 * k, k)
                 e.set_timing(True)
                 t0 = time.perf_counter()
-                counts = e.step_counted(a.steps * k, k)
+                if a.nocount:
+                    e.step(a.steps * k)
+                    counts = e.step_counted(0, k)
+                else:
+                    counts = e.step_counted(a.steps * k, k)
                 dt = time.perf_counter() - t0
                 t = e.timing()
                 h = e.hash()
             if ref is None:
                 ref = (h, counts.tolist())
-            line = {"board": a.board, "variant": name, "rep": rep, "k": k, "steps": a.steps,
+            line = {"board": a.board + ("-zero" if a.zero else ""), "variant": name + ("-nocount" if a.nocount else ""), "rep": rep, "k": k, "steps": a.steps,
                     "wall_ms_per_step": round(dt / a.steps * 1e3, 4), "step_ms": round(t["mean_ms"], 4),
                     "shard_steps": t["launches"], "TCUPS": round(H * W * k * a.steps / dt / 1e12, 2),
                     "same_result": (h, counts.tolist()) == ref}

@@ -35,7 +35,7 @@ STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear w
             a.slots[4 * i] = tl_c0; a.slots[4 * i + 1] = __builtin_amdgcn_s_memtime();
             a.slots[4 * i + 2] = prof_a; a.slots[4 * i + 3] = prof_b | ((uint64_t)wv << 56); (void)hw; (void)xcc;
 #else
-            a.slots[4 * i + 2] = hw; a.slots[4 * i + 3] = xcc;
+            a.slots[4 * i + 2] = hw; a.slots[4 * i + 3] = xcc | ((uint64_t)wv << 56) | ((uint64_t)(threadIdx.x >> 6) << 48);
 #endif
         }
         (void)alive;
@@ -128,7 +128,7 @@ def run(workload, strip):
     base = t0.min()
     s, e = (t0 - base) / 100.0, (t1 - base) / 100.0  # microseconds (100 MHz)
     span = e.max()
-    hw, xcc = v[:, 2], v[:, 3]
+    hw, xcc = v[:, 2], v[:, 3] & 0xFFFF
     cu = (hw >> 8) & 0xF
     se = (hw >> 13) & 0x7
     simd = (hw >> 4) & 0x3
@@ -146,6 +146,23 @@ def run(workload, strip):
            "cus_used": len(per_cu), "waves_per_cu": sorted({c for c, _ in per_cu.values()}),
            "cu_end_us_pct": [round(float(np.percentile([x for _, x in per_cu.values()], q)), 1) for q in (0, 10, 50, 90, 100)],
            "simd_hist": np.bincount(simd, minlength=4).tolist()}
+    if not os.environ.get("GOL_TL_PROF"):
+        # pipeline roles per SIMD (role = wv, the wave's position in its pipeline) and how the
+        # wave index maps to the SIMD
+        role = (v[:, 3] >> 56) & 0xFF
+        widx = (v[:, 3] >> 48) & 0xFF
+        out["simd_of_wave_index"] = {int(w): np.bincount(simd[widx == w], minlength=4).tolist() for w in np.unique(widx)}
+        # for every CU: at each wave's start, the roles resident on its SIMD (same CU) -- the
+        # fraction of waves that share their SIMD with another wave of the same role
+        same = 0
+        order = np.argsort(s)
+        for kk in np.unique(key):
+            idx = np.where(key == kk)[0]
+            for i in idx:
+                live = idx[(s[idx] <= s[i]) & (e[idx] > s[i]) & (simd[idx] == simd[i]) & (idx != i)]
+                same += int((role[live] == role[i]).any())
+        out["share_simd_with_same_role"] = round(same / len(v), 3)
+        out["role_simd_hist"] = {int(r): np.bincount(simd[role == r], minlength=4).tolist() for r in np.unique(role)}
     if os.environ.get("GOL_TL_PROF"):  # prof build: slots = (c0, c1, ready-wait, free-wait | role << 56) in shader cycles
         life_c = (v[:, 1] - v[:, 0]).astype(np.float64)
         role = (v[:, 3] >> 56) & 0xFF
