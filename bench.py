@@ -229,7 +229,10 @@ def roofline(kind, launch_ms, cell_updates, pmc, pmc_note):
                   "profile_clock_GHz": pmc.get("clock_GHz"),
                   "frac_at_profile_clock": round(ach / (VALU_PEAK_GINST / 2.4 * pmc["clock_GHz"]), 4)
                   if pmc.get("clock_GHz") else None,
-                  "cell_updates_per_valu_lane_op": round(cell_updates / (valu * 64), 3)})
+                  "cell_updates_per_valu_lane_op": round(cell_updates / (valu * 64), 3),
+                  "note": "VALU issue of the kernel's own instruction stream; since round 3 a band-layout "
+                          "generation is 9 logic ops per 32 cells (10 before, DESIGN.md §4.1), so the same "
+                          "frac means ~10 % more cell-updates/s"})
     else:  # no PMC profile of this kernel build: only the HBM side can be stated (None without traffic)
         r.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": hbm["frac"]})
