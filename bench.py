@@ -56,6 +56,9 @@ def parse(argv=None):
                          "(12 band / 8 standard), 32 for byte16k")
     ap.add_argument("--strip", type=int, default=0, help="rows per strip (0 = auto)")
     ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"])
+    ap.add_argument("--persist", action="store_true",
+                    help="the persistent multi-round launch (GOL_STEP_PERSIST) of a one-shard band board instead "
+                         "of one launch per step (A/B of DESIGN.md §4.7)")
     ap.add_argument("--cpl", type=int, default=0, choices=[0, 32, 64, 128],
                     help="cells per lane of the bit kernels (0 = library default: 128 on the band layout)")
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
@@ -289,7 +292,7 @@ def run_bits(args, ranks):
         # test mode: every rank an independent 1-GPU replica of rows_per_gpu rows
         H, sharded = H // world, False
     kw = dict(device=ranks.local, turns_per_launch=args.k, strip_rows=args.strip, layout=args.layout,
-              cells_per_lane=args.cpl)
+              cells_per_lane=args.cpl, persist=args.persist)
     if sharded and world > 1:
         uid = ranks.share(golhip.engine.rccl_unique_id() if rank == 0 else None)
         e = golhip.Engine.rank(H, W, world, rank, uid, **kw)

@@ -111,6 +111,8 @@ static void shard_release(gol_shard &s)
         if (b) (void)hipFree(b);
     free_exact_bytes(s);
     if (s.slots) (void)hipFree(s.slots);
+    if (s.pctl) (void)hipFree(s.pctl);
+    if (s.pslots) (void)hipFree(s.pslots);
     if (s.counts) (void)hipFree(s.counts);
     if (s.flag) (void)hipFree(s.flag);
     if (s.err) (void)hipFree(s.err);
@@ -181,6 +183,7 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
     e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
     if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
     e->step_flags = cfg ? (cfg->flags & (GOL_STEP_SERIAL | GOL_STEP_EDGE_FIRST | GOL_STEP_OVERLAP)) : 0;
+    e->persist = cfg && (cfg->flags & GOL_STEP_PERSIST);
     return GOL_OK;
 }
 
@@ -355,6 +358,7 @@ static int sync_all(gol_engine *e)
         for (auto &s : e->sh) {
             RCCHK(set_dev(s.device));
             HIPCHK(hipMemsetAsync(s.err, 0, sizeof(uint32_t), s.stream));
+            s.slots_zero = false;  // a faulted launch may have left counts in them
             // a timed-out pair may have left its claims set: this engine's streams only
             HIPCHK(golk_reset_claims(s.stream));
             HIPCHK(golk_reset_claims(s.edge));
@@ -437,8 +441,19 @@ static int plan_of(gol_engine *e, int i, gol_halo_op (&ops)[4])
 // s from shard p gets p's n-th send to s), so the one-GPU loopback tests exercise the RCCL
 // matching of the same plan, including nranks = 2 (one peer on both sides) and the one-shard
 // torus wrap (a shard sending to itself).
+// One shard that is the whole torus (LOCAL transport): the step launches read the wrap rows from
+// the board itself (step_launch), so there is nothing to exchange.
+static bool local_wrap(const gol_engine *e)
+{
+    return e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;
+}
+
 static int exchange(gol_engine *e)
 {
+    if (local_wrap(e)) {
+        e->halo_issued = false;
+        return GOL_OK;
+    }
     const int n = (int)e->sh.size();
     const int c = e->cur;
     const int64_t P = e->pitch;
@@ -524,7 +539,11 @@ static int step_launch(gol_engine *e, gol_shard &s, hipStream_t st, int k, int64
 {
     if (rows <= 0) return GOL_OK;
     uint32_t *mid = s.bits[e->cur];
-    const uint32_t *top = mid - (int64_t)k * e->pitch, *bot = mid + s.R * e->pitch;
+    const uint32_t *top = mid - (int64_t)k * e->pitch, *bot = mid + s.R * e->pitch;  // the ghost rows
+    if (local_wrap(e)) {  // the torus wrap straight from the board: rows R-k .. R-1 above, 0 .. k-1 below
+        top = mid + (s.R - k) * e->pitch;
+        bot = mid;
+    }
     uint32_t *dst = s.bits[1 - e->cur];
     if (e->band)
         HIPCHK(golk_band_step(top, mid, bot, dst, s.R, e->Wd, e->pitch, row0, rows, k, e->band_dw, e->strip, slots, s.err, st));
@@ -545,7 +564,7 @@ static int fold_timing(gol_engine *e)
         HIPCHK(hipEventElapsedTime(&x, s.tev[t.ev], s.tev[t.ev + 1]));
         e->t_ms += x;
         e->t_cells += t.cell_updates;
-        e->t_n += 1;
+        e->t_n += t.steps;
     }
     e->timed.clear();
     for (auto &s : e->sh) s.tused = 0;
@@ -562,6 +581,38 @@ static int timing_event(gol_engine *e, gol_shard &s, size_t *ev)
     }
     *ev = s.tused;
     s.tused += 2;
+    return GOL_OK;
+}
+
+// Timing of one stepping call (gol_engine_set_timing): one event pair per shard on its compute
+// stream around all the call's launches (per-launch events cost the GPU ~10-30 us each, a large
+// share of a 0.4 ms step), averaged over its steps by gol_engine_timing.
+static int timing_begin(gol_engine *e)
+{
+    if (!e->timing) return GOL_OK;
+    e->tcall_ev.assign(e->sh.size(), 0);
+    e->tcall_cells.assign(e->sh.size(), 0.0);
+    e->tcall_steps = 0;
+    for (size_t i = 0; i < e->sh.size(); ++i) {
+        gol_shard &s = e->sh[i];
+        RCCHK(set_dev(s.device));
+        RCCHK(timing_event(e, s, &e->tcall_ev[i]));
+        HIPCHK(hipEventRecord(s.tev[e->tcall_ev[i]], s.stream));
+    }
+    return GOL_OK;
+}
+
+static int timing_end(gol_engine *e)
+{
+    if (!e->timing || e->tcall_ev.size() != e->sh.size()) return GOL_OK;
+    for (size_t i = 0; i < e->sh.size(); ++i) {
+        gol_shard &s = e->sh[i];
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));  // (edge launches of the last step)
+        HIPCHK(hipEventRecord(s.tev[e->tcall_ev[i] + 1], s.stream));
+        if (e->tcall_steps > 0) e->timed.push_back({(int)i, e->tcall_ev[i], e->tcall_cells[i], e->tcall_steps});
+    }
+    e->tcall_ev.clear();
     return GOL_OK;
 }
 
@@ -593,12 +644,9 @@ static int launch_k(gol_engine *e, int k, bool count)
         int32_t np = 0;
         RCCHK(gol_step_plan(s.R, k, e->kx, step_mode(e, s, k), plan, 3, &np));
         uint64_t *slots = count ? s.slots : nullptr;
-        if (count) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
-        size_t ev = 0;
-        if (e->timing) {
-            RCCHK(timing_event(e, s, &ev));
-            HIPCHK(hipEventRecord(s.tev[ev], s.stream));
-        }
+        if (count && !s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        if (count) s.slots_zero = false;
+        if (e->timing) e->tcall_cells[i] += (double)s.R * (double)e->W * k;
         HIPCHK(hipEventRecord(s.ev_start, s.stream));  // the step's inputs are complete, slots zeroed
         bool edge_used = false, waited[2] = {false, false};
         int last_halo = -1;  // the last launch that reads the halo writes the rows the exchange sends
@@ -620,15 +668,83 @@ static int launch_k(gol_engine *e, int k, bool count)
             if (j == last_halo) HIPCHK(hipEventRecord(s.ev_edge, st));
         }
         if (edge_used) HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
-        if (e->timing) {
-            HIPCHK(hipEventRecord(s.tev[ev + 1], s.stream));
-            e->timed.push_back({i, ev, (double)s.R * (double)e->W * k});
-        }
     }
+    if (e->timing) e->tcall_steps += 1;
     e->cur = 1 - e->cur;
     // the next step's halo: waits only for each shard's ev_edge
     RCCHK(exchange(e));
     e->halo_ok = true;
+    return GOL_OK;
+}
+
+// ------------------------------------------------------------------ persistent multi-round steps
+// One shard that is the whole torus, stepped in the band layout at k = 12: many steps in one
+// launch (golk_band_persist: resident workgroups claim tiles round by round, each waiting only for
+// its 3 x 3 neighbourhood of the previous round).  It saves the kernel boundary and the drain of
+// the last round of workgroups at every step, which a board that fills the device only a few
+// times over pays in full.  The rows wrap inside the shard: no ghost rows, no
+// exchange.
+static bool persist_ok(gol_engine *e)
+{
+    if (!e->persist || e->sh.size() != 1 || e->nranks != 1 || e->mode != GOL_MODE_BITS || !e->band_capable ||
+        e->band_dw != 4 || e->k < GOL_DEFAULT_BAND_K || e->min_rows < GOL_DEFAULT_BAND_K)
+        return false;
+    int32_t strip = 0, ng = 0, ns = 0;
+    return golk_persist_geom(e->sh[0].R, e->Wd, e->strip, &strip, &ng, &ns);
+}
+
+// `rounds` k = 12 steps of the band board in one launch; count_every > 0: the alive count after
+// every count_every-th step into slot array i of `slots` (zeroed here).
+static int launch_persist(gol_engine *e, int64_t rounds, int count_every, uint64_t *slots, int64_t ncounts)
+{
+    gol_shard &s = e->sh[0];
+    RCCHK(set_dev(s.device));
+    int32_t strip = 0, ng = 0, ns = 0;
+    if (!golk_persist_geom(s.R, e->Wd, e->strip, &strip, &ng, &ns))
+        return gol_set_error(GOL_EINVAL, "persistent launch: board does not tile");
+    const int64_t words = golk_persist_ctl_words((int64_t)ng * ns);
+    if (s.pctl_words < words) {
+        if (s.pctl) (void)hipFree(s.pctl);
+        s.pctl = nullptr;
+        s.pctl_words = 0;
+        HIPCHK(hipMalloc(&s.pctl, words * sizeof(uint32_t)));
+        s.pctl_words = words;
+    }
+    RCCHK(invalidate_halo(e));  // an exchange still in flight reads rows the launch writes
+    if (slots && !(slots == s.slots && s.slots_zero)) HIPCHK(hipMemsetAsync(slots, 0, (size_t)ncounts * SLOT_BYTES, s.stream));
+    if (slots == s.slots) s.slots_zero = false;
+    if (e->timing) {
+        e->tcall_cells[0] += (double)s.R * (double)e->W * GOL_DEFAULT_BAND_K * rounds;
+        e->tcall_steps += rounds;
+    }
+    HIPCHK(golk_band_persist(s.bits[e->cur], s.bits[1 - e->cur], s.R, e->Wd, e->pitch, (int)rounds, e->strip,
+                             slots ? count_every : 0, s.pctl, slots, s.err, s.stream));
+#ifdef GOL_PERSIST_STATS  // measurement builds: the kernel's wait counters (gol_kernels.hip), one line per launch
+    {
+        uint32_t c[16];
+        HIPCHK(hipMemcpyAsync(c, s.pctl, sizeof c, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        const uint64_t *q = (const uint64_t *)(c + 2);
+        fprintf(stderr, "persist-stats rounds %lld tiles/round %d strip %d: pads %u fast %u | us: dep %.0f "
+                "wait loader %.0f middle %.0f storer %.0f life %.0f\n", (long long)rounds, ng * ns, strip, c[1], c[14],
+                q[0] / 100.0, q[1] / 100.0, q[2] / 100.0, q[3] / 100.0, q[4] / 100.0);
+    }
+#endif
+    e->cur = (e->cur + (int)(rounds & 1)) & 1;
+    e->turn += GOL_DEFAULT_BAND_K * rounds;
+    e->halo_ok = false;  // the ghost rows are not maintained by the persistent kernel
+    return GOL_OK;
+}
+
+// The per-shard slot arrays of a persistent launch with n count points.
+static int ensure_pslots(gol_shard &s, int64_t n)
+{
+    if (s.pslots_n >= n) return GOL_OK;
+    if (s.pslots) (void)hipFree(s.pslots);
+    s.pslots = nullptr;
+    s.pslots_n = 0;
+    HIPCHK(hipMalloc(&s.pslots, (size_t)n * SLOT_BYTES));
+    s.pslots_n = n;
     return GOL_OK;
 }
 
@@ -653,7 +769,8 @@ static int count_into_slots(gol_engine *e)
 {
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
-        HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        if (!s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        s.slots_zero = false;
         if (e->mode == GOL_MODE_BITS)
             HIPCHK(golk_popcount(s.bits[e->cur], s.R, e->Wd, e->pitch, s.slots, s.stream));
         else if (e->mode == GOL_MODE_EXACT)
@@ -684,7 +801,8 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
                 // 0/255 byte board: k turns per launch on the bytes (torus wrap through top/bot)
                 const int k = e->k >= 32 && n >= 32 && e->H >= 32 ? 32 : pick_k(e->k, n, e->H, 1, false);
                 const bool last = n == k && ci >= 0;
-                if (last) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+                if (last && !s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+                if (last) s.slots_zero = false;
                 HIPCHK(golk_bytes_blocked(mid + (e->H - k) * e->bstride, mid, mid, s.bytes[1 - e->bcur], e->H, e->W,
                                           e->bstride, 0, e->H, k, e->strip, last ? s.slots : nullptr, s.err, s.stream));
                 e->bcur = 1 - e->bcur;
@@ -701,6 +819,14 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
             continue;
         }
         if (e->band_capable) RCCHK(convert(e, true));
+        if (n >= GOL_DEFAULT_BAND_K && persist_ok(e)) {  // many steps in one launch
+            const int64_t rounds = std::min<int64_t>(n / GOL_DEFAULT_BAND_K, GOL_PERSIST_MAX_ROUNDS);
+            const bool last = rounds * GOL_DEFAULT_BAND_K == n && ci >= 0;  // its count: after the last round
+            RCCHK(launch_persist(e, rounds, (int)rounds, last ? e->sh[0].slots : nullptr, 1));
+            n -= rounds * GOL_DEFAULT_BAND_K;
+            counted = last;
+            continue;
+        }
         const int k = pick_k(e->k, n, e->min_rows, e->band ? e->band_dw : e->dw, e->band);
         const bool last = n == k && ci >= 0;
         RCCHK(launch_k(e, k, last));
@@ -713,6 +839,7 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
         for (auto &s : e->sh) {
             RCCHK(set_dev(s.device));
             HIPCHK(golk_slots_reduce(s.slots, 1, s.counts + ci, s.stream));
+            s.slots_zero = true;
         }
     }
     return GOL_OK;
@@ -723,7 +850,10 @@ int gol_engine_step_async(gol_engine *e, int64_t turns) { return advance(e, turn
 extern "C" int gol_engine_step(gol_engine *e, int64_t turns)
 {
     if (!e || turns < 0) return gol_set_error(GOL_EINVAL, "bad step arguments");
-    const int rc = advance(e, turns, -1);
+    RCCHK(timing_begin(e));
+    int rc = advance(e, turns, -1);
+    const int rt = timing_end(e);
+    if (!rc) rc = rt;
     const int rs = sync_all(e);
     return rc ? rc : rs;
 }
@@ -759,14 +889,33 @@ extern "C" int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t eve
         RCCHK(set_dev(s.device));
         RCCHK(ensure_counts(s, n));
     }
-    int rc = GOL_OK;
+    int rc = timing_begin(e);
     int64_t left = turns, ci = 0;
+    // counts every k = 12 steps or a multiple: the persistent launch counts inside (one slot array
+    // per count point, reduced on the device in one launch per chunk)
+    if (e->mode == GOL_MODE_BITS && e->band_capable && every % GOL_DEFAULT_BAND_K == 0 && n > 0) {
+        rc = convert(e, true);
+        if (rc == GOL_OK && persist_ok(e)) {
+            const int64_t per = every / GOL_DEFAULT_BAND_K;  // rounds per count point
+            gol_shard &s = e->sh[0];
+            while (ci < n && rc == GOL_OK) {
+                const int64_t chunk = std::min<int64_t>(n - ci, std::max<int64_t>(1, GOL_PERSIST_MAX_ROUNDS / per));
+                rc = ensure_pslots(s, chunk);
+                if (rc == GOL_OK) rc = launch_persist(e, chunk * per, (int)per, s.pslots, chunk);
+                if (rc == GOL_OK && golk_slots_reduce(s.pslots, chunk, s.counts + ci, s.stream) != hipSuccess)
+                    rc = gol_set_error(GOL_EHIP, "slots reduce failed");
+                ci += chunk;
+                left -= chunk * every;
+            }
+        }
+    }
     while (left > 0 && rc == GOL_OK) {
         const int64_t seg = std::min(every, left);
         rc = advance(e, seg, seg == every ? ci : -1);
         if (seg == every) ++ci;
         left -= seg;
     }
+    if (rc == GOL_OK) rc = timing_end(e);
     if (rc != GOL_OK) {
         (void)sync_all(e);
         return rc;
@@ -793,6 +942,7 @@ extern "C" int gol_engine_alive_count(gol_engine *e, uint64_t *count)
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         HIPCHK(golk_slots_reduce(s.slots, 1, s.counts, s.stream));
+        s.slots_zero = true;
     }
     return collect_counts(e, 1, count);
 }
@@ -805,7 +955,8 @@ extern "C" int gol_engine_hash(gol_engine *e, uint64_t *hash)
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         RCCHK(ensure_counts(s, 1));
-        HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        if (!s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
+        s.slots_zero = false;
         const uint32_t *bits = s.bits[e->cur];
         if (e->mode == GOL_MODE_EXACT) {  // loaded non-binary bytes at turn 0: hash the 255-cells
             HIPCHK(golk_pack(s.bytes[0] + e->bstride, s.R, e->W, e->bstride, s.bits[0], e->pitch, nullptr, s.stream));
@@ -813,6 +964,7 @@ extern "C" int gol_engine_hash(gol_engine *e, uint64_t *hash)
         }
         HIPCHK(golk_hash(bits, s.R, s.y0, e->Wd, e->pitch, s.slots, s.stream));
         HIPCHK(golk_slots_reduce(s.slots, 1, s.counts, s.stream));
+        s.slots_zero = true;
     }
     return collect_counts(e, 1, hash);
 }

@@ -24,6 +24,10 @@
 // so the kernels address input row y as board + y*pitch for -k <= y < R + k.
 #define GOL_GHOST_ROWS 16
 
+// Steps (rounds) of one persistent multi-round launch at most (a launch of the 2^17 x 2^20 board
+// runs ~12 ms per round).
+#define GOL_PERSIST_MAX_ROUNDS 64
+
 // Timing events per shard before the recorded steps are folded into running sums.
 #define GOL_TIMING_EVENTS 512
 
@@ -43,6 +47,7 @@ struct gol_shard {
     // y0-1 .. y1 (R + 2 rows, the halo rows from the host board), bytes[1] = R output rows.
     uint8_t *bytes[2] = {nullptr, nullptr};
     uint64_t *slots = nullptr;        // GOL_COUNT_SLOTS * 8 reduction slots
+    bool slots_zero = false;          // zeroed by the last slots reduce (no memset before the next count)
     uint64_t *counts = nullptr;       // per-count-point alive counts (step_counted)
     int64_t counts_cap = 0;
     uint32_t *flag = nullptr;         // nonbinary flag of a load
@@ -52,6 +57,12 @@ struct gol_shard {
     uint8_t *host_staging = nullptr;  // pinned host rows
     int64_t stage_rows = 0;
     ncclComm_t nccl = nullptr;
+    // persistent multi-round launches (gol_kernels.h golk_band_persist): claim / done words and
+    // the count slot arrays of one launch
+    uint32_t *pctl = nullptr;
+    int64_t pctl_words = 0;
+    uint64_t *pslots = nullptr;
+    int64_t pslots_n = 0;
     // timing (gol_engine_set_timing): events on `stream` around the timed launches
     std::vector<hipEvent_t> tev;
     size_t tused = 0;
@@ -67,6 +78,7 @@ struct gol_timed {
     int shard;
     size_t ev;  // index of the start event in the shard's pool (stop = ev + 1)
     double cell_updates;
+    int64_t steps;  // k-turn steps between the two events (a persistent launch runs many)
 };
 
 struct gol_engine {
@@ -93,10 +105,14 @@ struct gol_engine {
     int strip = 0;
     int kx = 1;                // halo rows of every exchange (>= the k of any step; gol_step_plan)
     int step_flags = 0;        // GOL_STEP_SERIAL
+    bool persist = false;      // one shard, band k = 12: many steps per launch (GOL_STEP_PERSIST)
     bool halo_ok = false;      // the ghost rows of bits[cur] hold the current halo (kx rows)
     bool halo_issued = false;  // an exchange was enqueued since the last synchronisation point
     bool timing = false;
     std::vector<gol_timed> timed;
+    std::vector<size_t> tcall_ev;      // the current stepping call's start events (one per shard)
+    std::vector<double> tcall_cells;   // and its cell-updates per shard
+    int64_t tcall_steps = 0;           // and its k-turn steps
     double t_ms = 0, t_cells = 0;  // folded timing sums (timed pool recycled)
     int64_t t_n = 0;
 };

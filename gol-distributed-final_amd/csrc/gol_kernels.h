@@ -40,6 +40,17 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
                           uint64_t *slots, uint32_t *err, hipStream_t s);
 int golk_band_useful_words(int k, int dw);
+// Persistent multi-round band pipeline: `rounds` k = 12 steps of one shard that is the whole
+// torus (rows wrap inside the shard, no ghost rows) in one launch; round r reads buf[r & 1] of
+// (cur, other) and writes the other one, so the result is in cur when rounds is even.  Tiles of
+// `strip` rows (0 = automatic) x one column group.  count_every > 0: the alive count after every
+// count_every-th round into slot array i = (r + 1) / count_every - 1 of `slots` (zeroed by the
+// caller).  ctl: golk_persist_ctl_words(ngroups * nstrips) words, zeroed here on s.
+// golk_persist_geom: false when the board does not fit the tiling (the caller steps per launch).
+bool golk_persist_geom(int64_t R, int64_t Wd, int strip_req, int32_t *strip, int32_t *ngroups, int32_t *nstrips);
+int64_t golk_persist_ctl_words(int64_t tiles);
+hipError_t golk_band_persist(uint32_t *cur, uint32_t *other, int64_t R, int64_t Wd, int64_t pitch, int rounds, int strip,
+                             int count_every, uint32_t *ctl, uint64_t *slots, uint32_t *err, hipStream_t s);
 // Rounds of resident workgroups a step launch over `rows` rows makes (the band pipeline; other
 // kernels: 1e9, i.e. many); for the engine's choice of step plan.
 double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int strip);
@@ -56,8 +67,9 @@ hipError_t golk_random_fill(uint32_t *dst, int64_t rows, int64_t grow0, int64_t 
                             hipStream_t s);
 hipError_t golk_popcount(const uint32_t *src, int64_t rows, int64_t Wd, int64_t pitch, uint64_t *slots,
                          hipStream_t s);
-// out[i] = sum of the GOL_COUNT_SLOTS slots of slot array i (arrays of GOL_COUNT_SLOTS*8 uint64).
-hipError_t golk_slots_reduce(const uint64_t *slots, int64_t n, uint64_t *out, hipStream_t s);
+// out[i] = sum of the GOL_COUNT_SLOTS slots of slot array i (arrays of GOL_COUNT_SLOTS*8 uint64);
+// the slots are left zeroed.
+hipError_t golk_slots_reduce(uint64_t *slots, int64_t n, uint64_t *out, hipStream_t s);
 hipError_t golk_hash(const uint32_t *src, int64_t rows, int64_t grow0, int64_t Wd, int64_t pitch, uint64_t *slots,
                      hipStream_t s);
 hipError_t golk_count_bytes(const uint8_t *src, int64_t rows, int64_t W, int64_t stride, uint64_t *slots,

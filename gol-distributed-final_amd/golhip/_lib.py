@@ -30,6 +30,7 @@ TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "r
 TRANSPORT_NAMES = {GOL_TRANSPORT_LOOPBACK: "loopback", GOL_TRANSPORT_RCCL: "rccl", GOL_TRANSPORT_LOCAL: "local"}
 GOL_SHARDS_SAME_DEVICE = 1
 GOL_STEP_SERIAL, GOL_STEP_EDGE_FIRST, GOL_STEP_OVERLAP = 2, 4, 8
+GOL_STEP_PERSIST = 16
 STEP_MODES = {"auto": 0, "serial": GOL_STEP_SERIAL, "edge_first": GOL_STEP_EDGE_FIRST, "overlap": GOL_STEP_OVERLAP}
 GOL_HALO_SEND, GOL_HALO_RECV = 0, 1
 GOL_LAUNCH_MAIN, GOL_LAUNCH_EDGE = 0, 1

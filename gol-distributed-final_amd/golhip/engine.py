@@ -14,8 +14,8 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_WRITE_FN, LAYOUTS, STEP_MODES, TRANSPORT_NAMES,
-                   TRANSPORTS, GolError, check, gol_config, lib)
+from ._lib import (GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_STEP_PERSIST, GOL_WRITE_FN, LAYOUTS, STEP_MODES,
+                   TRANSPORT_NAMES, TRANSPORTS, GolError, check, gol_config, lib)
 
 
 def rccl_unique_id(library=None) -> bytes:
@@ -31,14 +31,17 @@ def rccl_unique_id(library=None) -> bytes:
 class Engine:
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
                  strip_rows: int = 0, device: int = -1, layout: str = "auto", shards: int = 1,
-                 transport: str = "auto", same_device: bool = False, step: str = "auto", library=None,
-                 _rank=None):
+                 transport: str = "auto", same_device: bool = False, step: str = "auto", persist: bool = False,
+                 library=None, _rank=None):
+        # persist=True: the persistent multi-round launch of a one-shard band board (GOL_STEP_PERSIST,
+        # DESIGN.md §4.7) instead of one launch per k-turn step
         self.H, self.W = int(height), int(width)
         self._L = library or lib()
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, strip_rows=strip_rows,
                          cells_per_lane=cells_per_lane, layout=LAYOUTS[layout], shards=shards,
                          transport=TRANSPORTS[transport],
-                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | STEP_MODES[step])
+                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | STEP_MODES[step] |
+                         (GOL_STEP_PERSIST if persist else 0))
         h = ctypes.c_void_p()
         if _rank is None:
             self._check(self._L.gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))

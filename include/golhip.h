@@ -116,6 +116,9 @@ typedef struct gol_engine gol_engine;
 #define GOL_STEP_SERIAL 2        /* one launch per shard and step, after the halo exchange (gol_step_plan) */
 #define GOL_STEP_EDGE_FIRST 4    /* the edge rows first on the compute stream, then the interior (gol_step_plan) */
 #define GOL_STEP_OVERLAP 8       /* the edge rows on the edge stream beside the interior (gol_step_plan) */
+#define GOL_STEP_PERSIST 16      /* one shard in the band layout at k = 12: many steps per launch (the
+                                    persistent multi-round kernel; measured slower or
+                                    equal, so opt-in) */
 typedef struct gol_config {
     int32_t device;           /* HIP device ordinal (first shard); -1 = current device */
     int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
