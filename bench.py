@@ -48,8 +48,12 @@ KERNEL_SRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernel
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default per workload: >= ~0.1 s of GPU work; weak 20)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (default per workload: >= ~0.1 s of GPU work, weak 20): the "
+                         "GPU's clocks settle during the first ~0.1-0.2 s of load, and 3 steps of the weak "
+                         "board (36 ms) left its first timed steps 2.6 %% slower (DESIGN.md §6)")
     ap.add_argument("--workload", default="weak", choices=["weak", "strong262k", "bit64k", "byte16k"])
     ap.add_argument("--k", type=int, default=0,
                     help="turns per launch (temporal blocking); 0 = library default for bit boards "
@@ -74,7 +78,12 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration only (no GPU): ranks, barriers and the JSON line, value 0")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank exits at once
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    # per-workload defaults: each timed region and each warmup >= ~0.1-0.25 s of GPU work
+    steps, warm = {"weak": (20, 20), "strong262k": (40, 20), "bit64k": (300, 100), "byte16k": (600, 200)}[a.workload]
+    a.steps = steps if a.steps is None else a.steps
+    a.warmup = warm if a.warmup is None else a.warmup
+    return a
 
 
 # ------------------------------------------------------------------ launcher
@@ -373,35 +382,37 @@ def run_bytes(args, ranks):
     a = kern.unpack(bits, W)
     b = torch.empty_like(a)
     del bits
-    slots = torch.zeros(256 * 8, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     k = max(kk for kk in (32, 16, 8, 4, 2, 1) if kk <= args.k)
-    pairs = []
+    # one zeroed slot array per counted step (the kernel's fused count lands in its own array: no
+    # memset between steps); the per-step sums are taken once, inside the timed region
+    nslots = 256 * 8
+    slots = torch.zeros((max(args.warmup, args.steps), nslots), dtype=torch.int64, device="cuda")
     cur = [a, b]
 
-    def step(timed):
+    def step(i):
         src, dst = cur
-        if timed:
-            s = torch.cuda.Event(enable_timing=True)
-            s.record()
         if k == 1:
             check(lib().gol_dev_bytes_step(src.data_ptr(), H, W, W, 0, H, dst.data_ptr(), W, stream))
         else:
-            slots.zero_()
             check(lib().gol_dev_bytes_step_k(src[H - k:].data_ptr(), src.data_ptr(), src.data_ptr(), dst.data_ptr(),
-                                             H, W, W, 0, H, k, args.strip, slots.data_ptr(), stream))
-        if timed:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            pairs.append((s, e))
+                                             H, W, W, 0, H, k, args.strip, slots[i].data_ptr(), stream))
         cur.reverse()
 
-    for _ in range(args.warmup):
-        step(False)
+    for i in range(args.warmup):
+        step(i)
+    # (the count's reduction below is loaded and run once here: a first use inside the timed region
+    # would load its code object there)
+    _ = slots[:1].view(1, 256, 8)[:, :, 0].sum(dim=1)
+    slots.zero_()
     ranks.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    ev0.record()
+    for i in range(args.steps):
+        step(i)
+    ev1.record()
+    counts = slots[:args.steps].view(args.steps, 256, 8)[:, :, 0].sum(dim=1) if k > 1 else None
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ranks.barrier()
@@ -409,8 +420,8 @@ def run_bytes(args, ranks):
     check(lib().gol_dev_error(ranks.local, ctypes.byref(flags)))
     dt = ranks.max(dt)
     value = H * W * ranks.world * k * args.steps / dt
-    kms = sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
-    alive = int(slots.view(256, 8)[:, 0].sum().item()) if k > 1 else None
+    kms = ev0.elapsed_time(ev1) / args.steps  # HIP events around the timed launches, per launch
+    alive = int(counts[-1].item()) if counts is not None else None
     pmc, note = load_pmc(f"byte16k:{H}x{W}:k{k}:bytes")
     roof = roofline("bytes", kms, float(H * W * k), pmc, note)
     cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k,
