@@ -624,6 +624,7 @@ static int timing_end(gol_engine *e)
 static int step_mode(gol_engine *e, const gol_shard &s, int k)
 {
     if (e->step_flags) return e->step_flags;
+    if (local_wrap(e)) return GOL_STEP_SERIAL;  // nothing to exchange, nothing to overlap
     const double rounds = golk_step_rounds(e->band, s.R, e->Wd, k, e->band ? e->band_dw : e->dw, e->strip);
     return rounds > GOL_OVERLAP_ROUNDS ? GOL_STEP_OVERLAP : GOL_STEP_SERIAL;
 }

@@ -737,9 +737,16 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
     return -1;
 }
 
-// Cache policy bits of the band pipeline's output stores (2 = nt, streaming).
+// Cache policy bits of the band pipeline's output stores (2 = nt, streaming) and input loads.
 #ifndef GOL_BAND_STORE_AUX
 #define GOL_BAND_STORE_AUX 2
+#endif
+#ifndef GOL_BAND_LOAD_AUX
+#define GOL_BAND_LOAD_AUX 0
+#endif
+// Measurement builds: issue priority per pipeline role (loader, middle, storer), 0 = none set.
+#ifndef GOL_BAND_ROLE_PRIO
+#define GOL_BAND_ROLE_PRIO 0, 0, 0
 #endif
 // Pipeline shape of k = 12 (measurement builds may change it): KW stages in each of P waves.
 #ifndef GOL_BAND_KW
@@ -827,7 +834,7 @@ band_pipe_kernel(BitsArgs a)
             y = y > last_in ? last_in : (y < first_in ? first_in : y);
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, GOL_BAND_LOAD_AUX);
         }
     };
 
@@ -1061,6 +1068,15 @@ band_pipe_kernel(BitsArgs a)
     auto run_role = [&](auto role_c) -> bool {
         return dir ? run(role_c, std::true_type()) : run(role_c, std::false_type());
     };
+    {
+        constexpr int prio[3] = {GOL_BAND_ROLE_PRIO};
+        if constexpr ((prio[0] | prio[1] | prio[2]) != 0) {
+            const int pr = wv == 0 ? prio[0] : (wv == P - 1 ? prio[2] : prio[1]);
+            if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+            else if (pr == 3) __builtin_amdgcn_s_setprio(3);
+        }
+    }
     bool ok;
     if (wv == 0) ok = run_role(std::integral_constant<int, 0>());
     else if (wv == P - 1) ok = run_role(std::integral_constant<int, 2>());
