@@ -443,9 +443,12 @@ static int plan_of(gol_engine *e, int i, gol_halo_op (&ops)[4])
 // torus wrap (a shard sending to itself).
 // One shard that is the whole torus (LOCAL transport): the step launches read the wrap rows from
 // the board itself (step_launch), so there is nothing to exchange.
+#ifndef GOL_LOCAL_WRAP  // (measurement builds: 0 = copy the wrap rows into the ghost rows, as for shards)
+#define GOL_LOCAL_WRAP 1
+#endif
 static bool local_wrap(const gol_engine *e)
 {
-    return e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;
+    return GOL_LOCAL_WRAP && e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;
 }
 
 static int exchange(gol_engine *e)
