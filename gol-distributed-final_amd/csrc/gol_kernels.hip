@@ -826,6 +826,8 @@ band_pipe_kernel(BitsArgs a)
 
     // wave 0: block b -> in_ring[b % NS] (global_load_lds).  The slot is an argument: a lambda
     // that captures a __shared__ array silently loses the kernel's host-side stub.
+    // (one row address per row: the byte pipeline's interior-block stepping measured −4 % here on
+    // 65536², equal on the weak board: the band loader is not bound by its scalar instructions)
     auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
@@ -834,7 +836,11 @@ band_pipe_kernel(BitsArgs a)
             y = y > last_in ? last_in : (y < first_in ? first_in : y);
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
+#ifndef GOL_EXP_NOLOAD  // (measurement builds only: -DGOL_EXP_NOLOAD drops the loads, results are garbage)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, GOL_BAND_LOAD_AUX);
+#else
+            (void)g;
+#endif
         }
     };
 
@@ -1908,7 +1914,31 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     auto out_row = [&](int t) { return dir >= 0 ? s0 + t - 2 * K : s1e - 1 + 2 * K - t; };
     // wave 0: block b -> an in_ring slot (the slot is an argument: a lambda that captures a
     // __shared__ array loses the kernel's host-side stub)
+    // Interior blocks (all three rows inside the shard and inside [first_in, last_in]: every block
+    // but the first and last few of a strip) take one row address and step it by a pitch; the
+    // others clamp and pick the row's segment per row (~25 scalar instructions per row, ~150 per
+    // block against the loader's ~400 VALU: same box, 16384^2 bytes +2.4 %)
+    // The loader calls stage_in for blocks 0, 1, 2, ... in order: the first row of the next block
+    // (st_y) and its address (st_g) are carried from call to call.
+    const int in_lo = max(first_in, 0), in_hi = min(last_in, R - 1);
+    const int64_t row_step = dir >= 0 ? (int64_t)pitch : -(int64_t)pitch;
+    int st_y = in_row(0);
+    const char *st_g = mid_b + (int64_t)st_y * pitch + lane_off;
     auto stage_in = [&](int b, uint32_t (*slot)[2][256]) {
+        const int y0 = st_y;
+        const char *g = st_g;
+        st_y += dir >= 0 ? 3 : -3;
+        st_g += 3 * row_step;
+        const int ylo = dir >= 0 ? y0 : y0 - 2, yhi = dir >= 0 ? y0 + 2 : y0;
+        if (ylo >= in_lo && yhi <= in_hi) {
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step), &slot[S][0][0], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), &slot[S][1][0], 16, 0,
+                                                 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int S = 0; S < 3; ++S) {
             int y = in_row(3 * b + S);
