@@ -165,8 +165,11 @@ struct Operations {
         running = true;
         // Threads only chose the slab split across workers (broker.go:135-206); results
         // do not depend on it.  Here the board stays resident and is stepped in chunks
-        // sized so that Retrieve / Pause / Quit are served within ~10 ms.
+        // sized so that Retrieve / Pause / Quit are served within ~10 ms.  The first chunk is
+        // ~2^31 cell-updates (~1 ms on a launch-bound small board, ~0.1 ms on a large one) instead
+        // of one turn, so a short Run does not ramp up through a synchronised step per doubling.
         int64_t chunk = 1;
+        while (chunk < 1024 && chunk * 2 * req.ImageHeight * req.ImageWidth <= (int64_t(1) << 31)) chunk *= 2;
         while (cTurn < req.Turns && rc == GOL_OK) {
             if (control(lk)) break;
             const int64_t n = std::min(chunk, req.Turns - cTurn);

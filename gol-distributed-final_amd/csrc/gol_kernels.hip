@@ -2557,6 +2557,11 @@ int golk_auto_strip(int64_t rows, int64_t ngroups, int k)
     if (strip > hi) strip = hi;
     int64_t lo = 8 * (int64_t)k;
     if (lo < 32) lo = 32;
+    // a board too small for ~512 strips of lo rows (the reference's images: 512^2 is one column
+    // group) is latency-bound: a launch lasts one wave's serial walk over strip + 2k rows, so
+    // ~512 short strips win (512^2, k = 8: strip 1-2 -> 2.3 us per turn, 64 -> 5.8;
+    // profiles/r03/r03q_small.jsonl)
+    if (rows * ngroups < lo * 512) lo = std::max<int64_t>(1, rows * ngroups / 512);
     if (strip < lo) strip = lo;
     if (strip > rows) strip = rows;
     if (strip < 1) strip = 1;
@@ -2914,11 +2919,21 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
     a.ngroups = (int)((Wd + U - 1) / U);
     if (dw == 4 && k == 12) {
         // one workgroup per (column group, strip): strips up to 1024 rows (measured best at k = 12)
-        a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP)
-                            : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(1024, rows * a.ngroups / 2048)));
+        // Boards with fewer than ~256 tiles of 8k rows are latency-bound (a launch lasts one
+        // pipeline's walk over strip + 2k rows): ~512 tiles of >= 2 rows instead, without the
+        // one-round rank split (1024^2: 2.6 us per turn vs 5.1 at 96 rows; 4096^2: 3.0 vs 5.2;
+        // 8192^2: 4.1 vs 5.3; 16384^2 keeps the rank split: 6.0 vs 6.4 with 96-row tiles;
+        // profiles/r03/r03q_small.jsonl)
+        const int64_t work = rows * a.ngroups;
+        const bool small = strip <= 0 && work < (int64_t)8 * k * 256;
+        if (small)
+            a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(2, work / 512));
+        else
+            a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP)
+                                : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(1024, rows * a.ngroups / 2048)));
         // the pipe kernel's stores address a strip as one buffer (32-bit range)
         a.strip = (int)std::max<int64_t>(1, std::min<int64_t>(a.strip, (int64_t(1) << 30) / (pitch * 4)));
-        return launch_band_pipe(contig, a, s, strip <= 0);
+        return launch_band_pipe(contig, a, s, strip <= 0 && !small);
     }
     a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP) : golk_auto_strip(rows, a.ngroups, k);
     dim3 grid((a.ngroups + 3) / 4, (int)((rows + a.strip - 1) / a.strip));

@@ -14,7 +14,7 @@ from ._lib import GolError, device_count, halo_plan, lib, step_plan  # noqa: F40
 from .broker import Operations  # noqa: F401
 from .engine import Engine, next_state_slab, partition_rows  # noqa: F401
 from .pgm import read_pgm, write_pgm_bytes  # noqa: F401
-from .stubs import Cell, Parameters, Request, Response  # noqa: F401
+from .stubs import Cell, CellList, Parameters, Request, Response  # noqa: F401
 from .worker import GameOfLifeOperations  # noqa: F401
 
 

@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 
 from ._lib import TRANSPORTS, check, gol_config, gol_request, gol_response, lib
-from .stubs import Cell, Request, Response
+from .stubs import CellList, Request, Response
 
 
 def _request(req: Request, keep: list) -> gol_request:
@@ -32,8 +32,8 @@ def _request(req: Request, keep: list) -> gol_request:
     return r
 
 
-def _cells(xy: np.ndarray, n: int) -> list:
-    return [Cell(int(x), int(y)) for x, y in xy[:n]]
+def _cells(xy: np.ndarray, n: int) -> CellList:
+    return CellList(xy[:n].copy())  # the copy lets the H*W-pair buffer go
 
 
 class Operations:

@@ -127,6 +127,24 @@ def test_stub_names_match_reference(G):
         assert hasattr(res, f)
 
 
+def test_cell_list_reads_as_cells(G):
+    """A Response's alive list (CellList over the device's (x, y) pairs) reads like the
+    reference's []util.Cell: length, indexing, slicing, iteration and equality."""
+    from golhip.stubs import Cell, CellList
+    xy = np.array([[3, 0], [0, 1], [7, 1], [2, 5]], dtype=np.int32)
+    cl = CellList(xy)
+    want = [Cell(3, 0), Cell(0, 1), Cell(7, 1), Cell(2, 5)]
+    assert len(cl) == 4 and list(cl) == want and cl == want and want == list(cl)
+    assert cl[0] == Cell(3, 0) and cl[-1] == Cell(2, 5) and cl[1].X == 0 and cl[1].Y == 1
+    assert cl[1:3] == want[1:3] and isinstance(cl[1:3], CellList)
+    assert cl != want[:3] and cl != [Cell(3, 0), Cell(0, 1), Cell(7, 1), Cell(2, 6)]
+    assert cl == CellList(xy.copy()) and Cell(7, 1) in cl and Cell(1, 7) not in cl
+    assert sorted(cl, key=lambda c: (c.Y, c.X)) == want
+    assert len(CellList()) == 0 and list(CellList()) == [] and CellList() == []
+    assert all(type(c.X) is int for c in cl)
+    np.testing.assert_array_equal(cl.array(), xy)
+
+
 def test_pipe_kernels_wait_before_reading_lds(tmp_path):
     """The pipe kernels' inline-asm LDS reads: no instruction may read a destination
     VGPR before its s_waitcnt (a compiler copy there read stale rows once:
