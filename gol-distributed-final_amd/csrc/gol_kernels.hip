@@ -748,6 +748,10 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
 #ifndef GOL_BAND_ROLE_PRIO
 #define GOL_BAND_ROLE_PRIO 0, 0, 0
 #endif
+// Skip the rule on each wave's fill blocks (0: measurement builds compute them).
+#ifndef GOL_BAND_FILLSKIP
+#define GOL_BAND_FILLSKIP 1
+#endif
 // Pipeline shape of k = 12 (measurement builds may change it): KW stages in each of P waves.
 #ifndef GOL_BAND_KW
 #define GOL_BAND_KW 3
@@ -959,10 +963,11 @@ band_pipe_kernel(BitsArgs a)
     lds_flag_wr(wv == 0 ? scratch : cns_addr, 0);  // one younger LDS operation for block 0's wait
     // readers: the block the loop is about to run exists (an empty paired stream ends at once)
     bool more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
-    auto step = [&](int b, auto u_c, auto role_c, auto dyn_c) -> bool {
+    auto step = [&](int b, auto u_c, auto role_c, auto dyn_c, auto skip_c) -> bool {
         constexpr int US = decltype(u_c)::value;
         constexpr int ROLE = decltype(role_c)::value;
         constexpr bool DYN = decltype(dyn_c)::value;
+        constexpr bool SKIP = decltype(skip_c)::value;  // a fill block: no rule (see run)
         constexpr bool LAST = ROLE == 2;
         uint32_t cur[DW];
         auto realign = [&]() {
@@ -980,7 +985,7 @@ band_pipe_kernel(BitsArgs a)
         }
         nextv = lds_rd128_issue_o<US * SB + RB>(src_base);
         realign();
-        compute(std::integral_constant<int, 0>(), cur);
+        if constexpr (!SKIP) compute(std::integral_constant<int, 0>(), cur);
         if constexpr (LAST) {
             emit(cur);
         } else {
@@ -996,7 +1001,7 @@ band_pipe_kernel(BitsArgs a)
         }
         nextv = lds_rd128_issue_o<US * SB + 2 * RB>(src_base);
         realign();
-        compute(std::integral_constant<int, 1>(), cur);
+        if constexpr (!SKIP) compute(std::integral_constant<int, 1>(), cur);
         if constexpr (LAST) emit(cur);
         else {
             if constexpr (ROWF) {  // rows < 3b + 1 written (row 3b's write is older than the row-2 read)
@@ -1030,7 +1035,7 @@ band_pipe_kernel(BitsArgs a)
             lds_flag_wr(cns_addr, b + 1);
         }
         realign();
-        compute(std::integral_constant<int, 2>(), cur);
+        if constexpr (!SKIP) compute(std::integral_constant<int, 2>(), cur);
         if constexpr (LAST) emit(cur);
         else {
             if constexpr (ROWF) {  // rows < 3b + 2 written
@@ -1048,6 +1053,23 @@ band_pipe_kernel(BitsArgs a)
         constexpr bool DYN = decltype(dyn_c)::value;
         int nb = DYN ? 0 : nblk3;
         int b = 0;
+        // Fill blocks: stage g's input is valid from stream step 2g on, and its state of the
+        // steps before 2g only feeds outputs of steps before 2g + 2, which no later stage uses
+        // (the last stage's rows before step 2K fall outside the strip).  A wave whose first
+        // stage is g0 = KW * wv therefore passes the blocks that end before step 2 g0
+        // (3b + 2 < 2 g0) on without the rule -- whole loop trips of them, in a loop of their
+        // own (a branch per block inside the main loop made the compiler spill).  Launches of
+        // many rounds only: same box, weak +0.5 %, 262144² +0.7 %, but the one-round ROWF
+        // launch (65536²) -2 % (profiles/r03/r03r_ab_fill.jsonl).
+        if constexpr (ROLE != 0 && GOL_BAND_FILLSKIP && !ROWF) {
+            const int nskip = (2 * KW * wv) / 3;
+            for (; b + 3 <= nskip; b += 3) {
+                if (!more) break;
+                if (!step(b, std::integral_constant<int, 0>(), role_c, dyn_c, std::true_type())) return false;
+                if (!step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c, std::true_type())) return false;
+                if (!step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c, std::true_type())) return false;
+            }
+        }
         for (;; b += 3) {
             if constexpr (ROLE == 0) {
                 if constexpr (DYN) nb += grant(__builtin_amdgcn_readfirstlane(pending));
@@ -1055,9 +1077,9 @@ band_pipe_kernel(BitsArgs a)
             } else {
                 if (!more) break;
             }
-            if (!step(b, std::integral_constant<int, 0>(), role_c, dyn_c)) return false;
-            if (!step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c)) return false;
-            if (!step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c)) return false;
+            if (!step(b, std::integral_constant<int, 0>(), role_c, dyn_c, std::false_type())) return false;
+            if (!step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c, std::false_type())) return false;
+            if (!step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c, std::false_type())) return false;
         }
         if constexpr (ROLE != 2) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
