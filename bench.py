@@ -60,9 +60,6 @@ def parse(argv=None):
                          "(12 band / 8 standard), 32 for byte16k")
     ap.add_argument("--strip", type=int, default=0, help="rows per strip (0 = auto)")
     ap.add_argument("--layout", default="auto", choices=["auto", "standard", "band"])
-    ap.add_argument("--persist", action="store_true",
-                    help="the persistent multi-round launch (GOL_STEP_PERSIST) of a one-shard band board instead "
-                         "of one launch per step (A/B of DESIGN.md §4.7)")
     ap.add_argument("--cpl", type=int, default=0, choices=[0, 32, 64, 128],
                     help="cells per lane of the bit kernels (0 = library default: 128 on the band layout)")
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
@@ -72,9 +69,9 @@ def parse(argv=None):
                     help="after the timed steps write the board as a P5 file here (every rank its own "
                          "rows, gol_engine_write_pgm: config 5's snapshot); reported, not part of value")
     ap.add_argument("--share-gpu", action="store_true",
-                    help="testing only: every rank uses cuda:0 and runs an independent replica of its "
-                         "rows (RCCL refuses two ranks on one GPU); exercises the launcher, barriers "
-                         "and max-over-ranks timing on a 1-GPU box")
+                    help="testing on a 1-GPU box: every rank uses cuda:0 and the sharded workloads (weak, "
+                         "strong262k) run the same rank engine over the IPC transport (HIP IPC halo pulls, "
+                         "host collectives) instead of RCCL, which refuses two ranks on one GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration only (no GPU): ranks, barriers and the JSON line, value 0")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank exits at once
@@ -297,16 +294,15 @@ def run_bits(args, ranks):
         H, W, sharded = 262144, 262144, True
     else:
         H, W, sharded = 65536, 65536, False
-    if args.share_gpu and sharded and world > 1:
-        # test mode: every rank an independent 1-GPU replica of rows_per_gpu rows
-        H, sharded = H // world, False
     kw = dict(device=ranks.local, turns_per_launch=args.k, strip_rows=args.strip, layout=args.layout,
-              cells_per_lane=args.cpl, persist=args.persist)
+              cells_per_lane=args.cpl)
     if sharded and world > 1:
-        uid = ranks.share(golhip.engine.rccl_unique_id() if rank == 0 else None)
-        e = golhip.Engine.rank(H, W, world, rank, uid, **kw)
+        # one process per GPU over RCCL; ranks sharing one GPU (testing) over the IPC transport
+        transport = "ipc" if args.share_gpu else "rccl"
+        uid = ranks.share(golhip.engine.unique_id(transport) if rank == 0 else None)
+        e = golhip.Engine.rank(H, W, world, rank, uid, transport=transport, **kw)
         topo = e.topology()
-        assert topo["nranks"] == world and topo["transport"] == "rccl", topo
+        assert topo["nranks"] == world and topo["transport"] == transport, topo
     else:
         e = golhip.Engine(H, W, **kw)
         topo = e.topology()

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "golhip.h"
+#include "gol_comm.h"
 #include "gol_internal.h"
 #include "gol_kernels.h"
 
@@ -111,11 +112,10 @@ static void shard_release(gol_shard &s)
         if (b) (void)hipFree(b);
     free_exact_bytes(s);
     if (s.slots) (void)hipFree(s.slots);
-    if (s.pctl) (void)hipFree(s.pctl);
-    if (s.pslots) (void)hipFree(s.pslots);
     if (s.counts) (void)hipFree(s.counts);
     if (s.flag) (void)hipFree(s.flag);
     if (s.err) (void)hipFree(s.err);
+    if (s.coll) (void)hipFree(s.coll);
     if (s.host_word) (void)hipHostFree(s.host_word);
     if (s.staging) (void)hipFree(s.staging);
     if (s.host_staging) (void)hipHostFree(s.host_staging);
@@ -137,7 +137,8 @@ static int shard_alloc(gol_engine *e, gol_shard &s)
     HIPCHK(hipMalloc(&s.slots, SLOT_BYTES));
     HIPCHK(hipMalloc(&s.flag, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&s.err, sizeof(uint32_t)));
-    HIPCHK(hipHostMalloc((void **)&s.host_word, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHK(hipMalloc(&s.coll, GOL_COLL_WORDS * sizeof(uint32_t)));
+    HIPCHK(hipHostMalloc((void **)&s.host_word, GOL_HOST_WORDS * sizeof(uint32_t), hipHostMallocDefault));
     // on the shard's stream: it is non-blocking, so a null-stream memset could still be running
     // when the first load or fill kernel writes the board
     HIPCHK(hipMemsetAsync(s.err, 0, sizeof(uint32_t), s.stream));
@@ -183,7 +184,6 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
     e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
     if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
     e->step_flags = cfg ? (cfg->flags & (GOL_STEP_SERIAL | GOL_STEP_EDGE_FIRST | GOL_STEP_OVERLAP)) : 0;
-    e->persist = cfg && (cfg->flags & GOL_STEP_PERSIST);
     return GOL_OK;
 }
 
@@ -283,8 +283,10 @@ extern "C" int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int3
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
     int transport = cfg ? cfg->transport : GOL_TRANSPORT_AUTO;
     if (transport == GOL_TRANSPORT_AUTO) transport = nranks > 1 ? GOL_TRANSPORT_RCCL : GOL_TRANSPORT_LOCAL;
-    if (rc == GOL_OK && transport != GOL_TRANSPORT_RCCL && !(transport == GOL_TRANSPORT_LOCAL && nranks == 1))
-        rc = gol_set_error(GOL_EINVAL, "ranks in several processes exchange halos over RCCL");
+    if (rc == GOL_OK && transport != GOL_TRANSPORT_RCCL && transport != GOL_TRANSPORT_IPC &&
+        !(transport == GOL_TRANSPORT_LOCAL && nranks == 1))
+        rc = gol_set_error(GOL_EINVAL, "ranks in several processes exchange halos over RCCL or IPC");
+    if (rc == GOL_OK && transport == GOL_TRANSPORT_IPC && !id) rc = gol_set_error(GOL_EINVAL, "the IPC transport needs an id");
     e->nranks = nranks;
     e->rank = rank;
     e->rank_mode = true;
@@ -296,6 +298,17 @@ extern "C" int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int3
         else if (ncclGetUniqueId(&u) != ncclSuccess) rc = gol_set_error(GOL_ECOMM, "ncclGetUniqueId failed");
         ncclResult_t r = rc == GOL_OK ? ncclCommInitRank(&e->sh[0].nccl, nranks, u, rank) : ncclSuccess;
         if (r != ncclSuccess) rc = gol_set_error(GOL_ECOMM, "ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(r));
+        if (rc == GOL_OK) e->comm = gol_comm_rccl(e->sh[0].nccl);
+    }
+    if (rc == GOL_OK && transport == GOL_TRANSPORT_IPC) {
+        // the ring neighbours this rank pulls its ghost rows from (gol_halo_plan's peers)
+        for (int p : {(rank + nranks - 1) % nranks, (rank + 1) % nranks})
+            if (p != rank && std::find(e->ipc_peers.begin(), e->ipc_peers.end(), p) == e->ipc_peers.end())
+                e->ipc_peers.push_back(p);
+        rc = set_dev(dev);
+        if (rc == GOL_OK)
+            rc = gol_ipc::open(id, nranks, rank, dev, H, W, e->sh[0].bits_alloc, e->ipc_peers, &e->ipc);
+        e->comm = e->ipc;
     }
     if (rc != GOL_OK) {
         gol_engine_destroy(e);
@@ -308,6 +321,12 @@ extern "C" int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int3
 extern "C" void gol_engine_destroy(gol_engine *e)
 {
     if (!e) return;
+    for (auto &s : e->sh) {  // (an IPC wait or signal may still read or write the flag words)
+        (void)hipSetDevice(s.device);
+        for (hipStream_t st : {s.stream, s.edge, s.comm})
+            if (st) (void)hipStreamSynchronize(st);
+    }
+    delete e->comm;  // the IPC transport unmaps the peers' buffers; RCCL's comm is the shard's
     for (auto &s : e->sh) shard_release(s);
     delete e;
 }
@@ -332,17 +351,24 @@ extern "C" int gol_engine_shard(gol_engine *e, int32_t i, int32_t *device, int64
 }
 
 // ------------------------------------------------------------------ synchronisation, errors
+// Ranks in several processes: whole-board calls are collective (gol_comm).
+static bool several(const gol_engine *e) { return e->rank_mode && e->nranks > 1; }
+
 // Wait for every shard's work and read the shards' device error words (one pinned readback
 // queued behind the work, so the check costs no extra synchronisation).
-// With ranks in several processes the error words are all-reduced first (ncclMax), so a fault
-// on one rank -- whose rows reach the others through the halo -- fails the call on every rank.
-static int sync_all(gol_engine *e)
+// With ranks in several processes the error words are all-reduced first (max), so a fault on
+// one rank -- whose rows reach the others through the halo -- fails the call on every rank; it
+// also ends every rank's halo copies (the IPC transport's all-reduce is a host barrier behind
+// the streams), so no rank reads a neighbour's buffers past this point.  `collective` = false:
+// this process's shards only (a call that other ranks do not make).
+static int sync_all(gol_engine *e, bool collective = true)
 {
-    const bool several = e->rank_mode && e->nranks > 1;
+    const bool coll = collective && several(e);
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));  // (the edge launches' error word writes)
-        if (several) NCCLCHK(ncclAllReduce(s.err, s.err, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.stream, s.ev_halo, 0));  // (the halo copies, the IPC waits' error word)
+        if (coll) RCCHK(e->comm->allreduce_max_u32(s.err, 1, s.stream));
         HIPCHK(hipMemcpyAsync(s.host_word, s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
     }
     uint32_t flags = 0;
@@ -362,12 +388,16 @@ static int sync_all(gol_engine *e)
             // a timed-out pair may have left its claims set: this engine's streams only
             HIPCHK(golk_reset_claims(s.stream));
             HIPCHK(golk_reset_claims(s.edge));
+            // a workgroup that gave up may not have freed its CU slot (role placement: speed only)
+            HIPCHK(golk_reset_cu_slots(s.device, s.stream));
             HIPCHK(hipStreamSynchronize(s.stream));
             HIPCHK(hipStreamSynchronize(s.edge));
         }
         e->halo_ok = false;
         return gol_set_error(GOL_EHIP, "device fault in a step kernel (error flags 0x%x: %s); the board is not valid",
-                             flags, (flags & GOLK_ERR_SPIN) ? "a pipeline wave timed out waiting for its neighbour" : "?");
+                             flags, (flags & GOLK_ERR_SPIN) ? "a pipeline wave timed out waiting for its neighbour"
+                                    : (flags & GOLK_ERR_IPC) ? "an IPC rank timed out waiting for a neighbour's halo rows"
+                                                             : "?");
     }
     if (e->mode == GOL_MODE_BITS)
         for (auto &s : e->sh) free_exact_bytes(s);  // the exact first turn's byte rows, once used
@@ -377,11 +407,35 @@ static int sync_all(gol_engine *e)
 // Collective barrier of the ranks of a several-process engine (a one-element all-reduce).
 static int rank_barrier(gol_engine *e)
 {
-    if (!e->rank_mode || e->nranks == 1) return GOL_OK;
+    if (!several(e)) return GOL_OK;
     gol_shard &s = e->sh[0];
     RCCHK(set_dev(s.device));
-    NCCLCHK(ncclAllReduce(s.flag, s.flag, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+    return e->comm->barrier(s.coll, s.stream);
+}
+
+// Before a stepping call with several ranks: the ranks agree on the board state, and any rank
+// whose halo is stale (its rows changed outside a step: load_words on that rank alone) makes
+// every rank exchange again, so the exchanges -- collective, paired in order -- stay matched.
+static int agree_step_state(gol_engine *e)
+{
+    if (!several(e)) return GOL_OK;
+    gol_shard &s = e->sh[0];
+    RCCHK(set_dev(s.device));
+    uint32_t *v = s.host_word + 4;  // [stale halo, mode, cur, band, ~mode, ~cur, ~band]: max of x and of ~x
+    const uint32_t st[3] = {(uint32_t)e->mode, (uint32_t)e->cur, (uint32_t)e->band};
+    v[0] = e->halo_ok ? 0u : 1u;
+    for (int i = 0; i < 3; ++i) {
+        v[1 + i] = st[i];
+        v[4 + i] = ~st[i];
+    }
+    HIPCHK(hipMemcpyAsync(s.coll, v, 7 * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
+    RCCHK(e->comm->allreduce_max_u32(s.coll, 7, s.stream));
+    HIPCHK(hipMemcpyAsync(v, s.coll, 7 * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
+    for (int i = 0; i < 3; ++i)
+        if (v[1 + i] != ~v[4 + i])
+            return gol_set_error(GOL_ESTATE, "the ranks disagree on the board state (mode / buffer / layout)");
+    if (v[0]) e->halo_ok = false;
     return GOL_OK;
 }
 
@@ -395,6 +449,8 @@ static int invalidate_halo(gol_engine *e)
             RCCHK(set_dev(s.device));
             HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
             for (auto &t : e->sh) HIPCHK(hipStreamWaitEvent(s.stream, t.ev_halo, 0));  // (loopback: t reads my rows)
+            // IPC: the neighbours have copied my rows of the last exchange out of my buffers
+            if (e->ipc) RCCHK(e->ipc->wait(s.stream, e->ipc_peers, GOL_IPC_PULLED, e->xn, s.err));
         }
     e->halo_ok = false;
     return GOL_OK;
@@ -443,12 +499,61 @@ static int plan_of(gol_engine *e, int i, gol_halo_op (&ops)[4])
 // torus wrap (a shard sending to itself).
 // One shard that is the whole torus (LOCAL transport): the step launches read the wrap rows from
 // the board itself (step_launch), so there is nothing to exchange.
-#ifndef GOL_LOCAL_WRAP  // (measurement builds: 0 = copy the wrap rows into the ghost rows, as for shards)
-#define GOL_LOCAL_WRAP 1
-#endif
 static bool local_wrap(const gol_engine *e)
 {
-    return GOL_LOCAL_WRAP && e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;
+    return e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;
+}
+
+// IPC transport (one shard per process): this rank's exchange xn on its comm stream, pulling
+// each ghost block out of the neighbour's HBM:
+//   1. signal READY = xn once the rows this rank sends are written (ev_edge);
+//   2. wait until each neighbour's READY has reached xn (its rows for this exchange are written);
+//   3. copy every receive of my gol_halo_plan from the peer's matching send (the peer's nth send
+//      to me for my nth receive from it: the pairing RCCL applies to the same plans);
+//   4. signal PULLED = xn.
+// A neighbour overwrites the rows it sent only in a later step's halo-reading launch, which
+// waits for its own exchange xn+1, i.e. for my READY xn+1, which I signal after my step's
+// halo-reading launches, which waited for my pulls of xn: so nothing else orders my copies
+// against its writes.  Writes outside a step wait for PULLED explicitly (invalidate_halo).
+static int exchange_ipc(gol_engine *e)
+{
+    gol_shard &s = e->sh[0];
+    RCCHK(set_dev(s.device));
+    const int c = e->cur;
+    const int64_t P = e->pitch;
+    const size_t hb = (size_t)e->kx * P * sizeof(uint32_t);
+    gol_halo_op mine[4];
+    RCCHK(plan_of(e, 0, mine));
+    const uint32_t xn = ++e->xn;
+    HIPCHK(hipStreamWaitEvent(s.comm, s.ev_edge, 0));
+    RCCHK(e->ipc->signal(s.comm, GOL_IPC_READY, xn));
+    RCCHK(e->ipc->wait(s.comm, e->ipc_peers, GOL_IPC_READY, xn, s.err));
+    for (int j = 0; j < 4; ++j) {
+        const gol_halo_op &rv = mine[j];
+        if (rv.kind != GOL_HALO_RECV) continue;
+        int nth = 0;  // this is my nth receive from rv.peer
+        for (int jj = 0; jj < j; ++jj) nth += mine[jj].kind == GOL_HALO_RECV && mine[jj].peer == rv.peer;
+        gol_halo_op theirs[4];
+        int32_t n = 0;
+        RCCHK(gol_halo_plan(e->H, e->nranks, rv.peer, e->kx, theirs, 4, &n));
+        const gol_halo_op *sd = nullptr;  // the peer's nth send to me
+        for (int m = 0, cnt = 0; m < n && !sd; ++m)
+            if (theirs[m].kind == GOL_HALO_SEND && theirs[m].peer == e->rank && cnt++ == nth) sd = &theirs[m];
+        if (!sd || sd->rows != rv.rows) return gol_set_error(GOL_EINVAL, "halo plan: unmatched receive");
+        const uint32_t *src;
+        if (rv.peer == e->rank) {
+            src = s.bits[c];
+        } else {
+            const uint32_t *base = e->ipc->peer_buf(rv.peer, c);
+            if (!base) return gol_set_error(GOL_ESTATE, "IPC: rank %d is not mapped", rv.peer);
+            src = base + (int64_t)GOL_GHOST_ROWS * P;  // row 0 of the peer's buffer
+        }
+        HIPCHK(hipMemcpyAsync(s.bits[c] + rv.row * P, src + sd->row * P, hb, hipMemcpyDeviceToDevice, s.comm));
+    }
+    RCCHK(e->ipc->signal(s.comm, GOL_IPC_PULLED, xn));
+    HIPCHK(hipEventRecord(s.ev_halo, s.comm));
+    e->halo_issued = true;
+    return GOL_OK;
 }
 
 static int exchange(gol_engine *e)
@@ -457,6 +562,7 @@ static int exchange(gol_engine *e)
         e->halo_issued = false;
         return GOL_OK;
     }
+    if (e->transport == GOL_TRANSPORT_IPC) return exchange_ipc(e);
     const int n = (int)e->sh.size();
     const int c = e->cur;
     const int64_t P = e->pitch;
@@ -605,9 +711,13 @@ static int timing_begin(gol_engine *e)
     return GOL_OK;
 }
 
+// A stepping call is being timed (timing_begin .. timing_end): launches outside such a call
+// (gol_engine_step_flips) are not.
+static bool timing_open(const gol_engine *e) { return e->timing && e->tcall_ev.size() == e->sh.size(); }
+
 static int timing_end(gol_engine *e)
 {
-    if (!e->timing || e->tcall_ev.size() != e->sh.size()) return GOL_OK;
+    if (!timing_open(e)) return GOL_OK;
     for (size_t i = 0; i < e->sh.size(); ++i) {
         gol_shard &s = e->sh[i];
         RCCHK(set_dev(s.device));
@@ -650,7 +760,7 @@ static int launch_k(gol_engine *e, int k, bool count)
         uint64_t *slots = count ? s.slots : nullptr;
         if (count && !s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
         if (count) s.slots_zero = false;
-        if (e->timing) e->tcall_cells[i] += (double)s.R * (double)e->W * k;
+        if (timing_open(e)) e->tcall_cells[i] += (double)s.R * (double)e->W * k;
         HIPCHK(hipEventRecord(s.ev_start, s.stream));  // the step's inputs are complete, slots zeroed
         bool edge_used = false, waited[2] = {false, false};
         int last_halo = -1;  // the last launch that reads the halo writes the rows the exchange sends
@@ -673,82 +783,11 @@ static int launch_k(gol_engine *e, int k, bool count)
         }
         if (edge_used) HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
     }
-    if (e->timing) e->tcall_steps += 1;
+    if (timing_open(e)) e->tcall_steps += 1;
     e->cur = 1 - e->cur;
     // the next step's halo: waits only for each shard's ev_edge
     RCCHK(exchange(e));
     e->halo_ok = true;
-    return GOL_OK;
-}
-
-// ------------------------------------------------------------------ persistent multi-round steps
-// One shard that is the whole torus, stepped in the band layout at k = 12: many steps in one
-// launch (golk_band_persist: resident workgroups claim tiles round by round, each waiting only for
-// its 3 x 3 neighbourhood of the previous round).  It saves the kernel boundary and the drain of
-// the last round of workgroups at every step, which a board that fills the device only a few
-// times over pays in full.  The rows wrap inside the shard: no ghost rows, no
-// exchange.
-static bool persist_ok(gol_engine *e)
-{
-    if (!e->persist || e->sh.size() != 1 || e->nranks != 1 || e->mode != GOL_MODE_BITS || !e->band_capable ||
-        e->band_dw != 4 || e->k < GOL_DEFAULT_BAND_K || e->min_rows < GOL_DEFAULT_BAND_K)
-        return false;
-    int32_t strip = 0, ng = 0, ns = 0;
-    return golk_persist_geom(e->sh[0].R, e->Wd, e->strip, &strip, &ng, &ns);
-}
-
-// `rounds` k = 12 steps of the band board in one launch; count_every > 0: the alive count after
-// every count_every-th step into slot array i of `slots` (zeroed here).
-static int launch_persist(gol_engine *e, int64_t rounds, int count_every, uint64_t *slots, int64_t ncounts)
-{
-    gol_shard &s = e->sh[0];
-    RCCHK(set_dev(s.device));
-    int32_t strip = 0, ng = 0, ns = 0;
-    if (!golk_persist_geom(s.R, e->Wd, e->strip, &strip, &ng, &ns))
-        return gol_set_error(GOL_EINVAL, "persistent launch: board does not tile");
-    const int64_t words = golk_persist_ctl_words((int64_t)ng * ns);
-    if (s.pctl_words < words) {
-        if (s.pctl) (void)hipFree(s.pctl);
-        s.pctl = nullptr;
-        s.pctl_words = 0;
-        HIPCHK(hipMalloc(&s.pctl, words * sizeof(uint32_t)));
-        s.pctl_words = words;
-    }
-    RCCHK(invalidate_halo(e));  // an exchange still in flight reads rows the launch writes
-    if (slots && !(slots == s.slots && s.slots_zero)) HIPCHK(hipMemsetAsync(slots, 0, (size_t)ncounts * SLOT_BYTES, s.stream));
-    if (slots == s.slots) s.slots_zero = false;
-    if (e->timing) {
-        e->tcall_cells[0] += (double)s.R * (double)e->W * GOL_DEFAULT_BAND_K * rounds;
-        e->tcall_steps += rounds;
-    }
-    HIPCHK(golk_band_persist(s.bits[e->cur], s.bits[1 - e->cur], s.R, e->Wd, e->pitch, (int)rounds, e->strip,
-                             slots ? count_every : 0, s.pctl, slots, s.err, s.stream));
-#ifdef GOL_PERSIST_STATS  // measurement builds: the kernel's wait counters (gol_kernels.hip), one line per launch
-    {
-        uint32_t c[16];
-        HIPCHK(hipMemcpyAsync(c, s.pctl, sizeof c, hipMemcpyDeviceToHost, s.stream));
-        HIPCHK(hipStreamSynchronize(s.stream));
-        const uint64_t *q = (const uint64_t *)(c + 2);
-        fprintf(stderr, "persist-stats rounds %lld tiles/round %d strip %d: pads %u fast %u | us: dep %.0f "
-                "wait loader %.0f middle %.0f storer %.0f life %.0f\n", (long long)rounds, ng * ns, strip, c[1], c[14],
-                q[0] / 100.0, q[1] / 100.0, q[2] / 100.0, q[3] / 100.0, q[4] / 100.0);
-    }
-#endif
-    e->cur = (e->cur + (int)(rounds & 1)) & 1;
-    e->turn += GOL_DEFAULT_BAND_K * rounds;
-    e->halo_ok = false;  // the ghost rows are not maintained by the persistent kernel
-    return GOL_OK;
-}
-
-// The per-shard slot arrays of a persistent launch with n count points.
-static int ensure_pslots(gol_shard &s, int64_t n)
-{
-    if (s.pslots_n >= n) return GOL_OK;
-    if (s.pslots) (void)hipFree(s.pslots);
-    s.pslots = nullptr;
-    s.pslots_n = 0;
-    HIPCHK(hipMalloc(&s.pslots, (size_t)n * SLOT_BYTES));
-    s.pslots_n = n;
     return GOL_OK;
 }
 
@@ -823,14 +862,6 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
             continue;
         }
         if (e->band_capable) RCCHK(convert(e, true));
-        if (n >= GOL_DEFAULT_BAND_K && persist_ok(e)) {  // many steps in one launch
-            const int64_t rounds = std::min<int64_t>(n / GOL_DEFAULT_BAND_K, GOL_PERSIST_MAX_ROUNDS);
-            const bool last = rounds * GOL_DEFAULT_BAND_K == n && ci >= 0;  // its count: after the last round
-            RCCHK(launch_persist(e, rounds, (int)rounds, last ? e->sh[0].slots : nullptr, 1));
-            n -= rounds * GOL_DEFAULT_BAND_K;
-            counted = last;
-            continue;
-        }
         const int k = pick_k(e->k, n, e->min_rows, e->band ? e->band_dw : e->dw, e->band);
         const bool last = n == k && ci >= 0;
         RCCHK(launch_k(e, k, last));
@@ -854,6 +885,7 @@ int gol_engine_step_async(gol_engine *e, int64_t turns) { return advance(e, turn
 extern "C" int gol_engine_step(gol_engine *e, int64_t turns)
 {
     if (!e || turns < 0) return gol_set_error(GOL_EINVAL, "bad step arguments");
+    RCCHK(agree_step_state(e));
     RCCHK(timing_begin(e));
     int rc = advance(e, turns, -1);
     const int rt = timing_end(e);
@@ -870,8 +902,7 @@ static int collect_counts(gol_engine *e, int64_t n, uint64_t *out)
     for (size_t i = 0; i < e->sh.size(); ++i) {
         gol_shard &s = e->sh[i];
         RCCHK(set_dev(s.device));
-        if (e->rank_mode && e->nranks > 1)
-            NCCLCHK(ncclAllReduce(s.counts, s.counts, n, ncclUint64, ncclSum, s.nccl, s.stream));
+        if (several(e)) RCCHK(e->comm->allreduce_sum_u64(s.counts, n, s.stream));
         HIPCHK(hipMemcpyAsync(tmp.data() + i * n, s.counts, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream));
     }
     RCCHK(sync_all(e));
@@ -893,26 +924,9 @@ extern "C" int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t eve
         RCCHK(set_dev(s.device));
         RCCHK(ensure_counts(s, n));
     }
+    RCCHK(agree_step_state(e));
     int rc = timing_begin(e);
     int64_t left = turns, ci = 0;
-    // counts every k = 12 steps or a multiple: the persistent launch counts inside (one slot array
-    // per count point, reduced on the device in one launch per chunk)
-    if (e->mode == GOL_MODE_BITS && e->band_capable && every % GOL_DEFAULT_BAND_K == 0 && n > 0) {
-        rc = convert(e, true);
-        if (rc == GOL_OK && persist_ok(e)) {
-            const int64_t per = every / GOL_DEFAULT_BAND_K;  // rounds per count point
-            gol_shard &s = e->sh[0];
-            while (ci < n && rc == GOL_OK) {
-                const int64_t chunk = std::min<int64_t>(n - ci, std::max<int64_t>(1, GOL_PERSIST_MAX_ROUNDS / per));
-                rc = ensure_pslots(s, chunk);
-                if (rc == GOL_OK) rc = launch_persist(e, chunk * per, (int)per, s.pslots, chunk);
-                if (rc == GOL_OK && golk_slots_reduce(s.pslots, chunk, s.counts + ci, s.stream) != hipSuccess)
-                    rc = gol_set_error(GOL_EHIP, "slots reduce failed");
-                ci += chunk;
-                left -= chunk * every;
-            }
-        }
-    }
     while (left > 0 && rc == GOL_OK) {
         const int64_t seg = std::min(every, left);
         rc = advance(e, seg, seg == every ? ci : -1);
@@ -990,7 +1004,7 @@ static int any_nonbinary(gol_engine *e, bool *out)
     uint32_t f = 0;
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
-        if (e->rank_mode && e->nranks > 1) NCCLCHK(ncclAllReduce(s.flag, s.flag, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+        if (several(e)) RCCHK(e->comm->allreduce_max_u32(s.flag, 1, s.stream));
         HIPCHK(hipMemcpyAsync(s.host_word + 1, s.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
     }
     for (auto &s : e->sh) {
@@ -1195,11 +1209,11 @@ static int load_pgm_impl(gol_engine *e, const FileRows &fr)
         }
         HIPCHK(hipStreamSynchronize(s.stream));
     }
-    if (e->rank_mode && e->nranks > 1) {  // agree on the verdict
+    if (several(e)) {  // agree on the verdict
         gol_shard &s = e->sh[0];
         s.host_word[2] = ws;
         HIPCHK(hipMemcpyAsync(s.flag, s.host_word + 2, sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
-        NCCLCHK(ncclAllReduce(s.flag, s.flag, 1, ncclUint32, ncclMax, s.nccl, s.stream));
+        RCCHK(e->comm->allreduce_max_u32(s.flag, 1, s.stream));
         HIPCHK(hipMemcpyAsync(s.host_word + 2, s.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
         HIPCHK(hipStreamSynchronize(s.stream));
         ws = s.host_word[2];
@@ -1335,6 +1349,7 @@ extern "C" int gol_engine_alive_cells(gol_engine *e, int32_t *xy, int64_t cap, i
 extern "C" int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, int64_t *n)
 {
     if (!e || !n || cap < 0 || (cap > 0 && !xy)) return gol_set_error(GOL_EINVAL, "bad arguments");
+    RCCHK(agree_step_state(e));
     RCCHK(ensure_standard(e));
     int64_t total = 0;
     if (e->mode == GOL_MODE_BITS) {
@@ -1573,7 +1588,7 @@ extern "C" int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *p
     if (!e || !bits || !pitch) return gol_set_error(GOL_EINVAL, "bad arguments");
     if (e->mode != GOL_MODE_BITS) return gol_set_error(GOL_ESTATE, "board is not bit-resident");
     RCCHK(ensure_standard(e));
-    RCCHK(sync_all(e));
+    RCCHK(sync_all(e, false));
     *bits = e->sh[0].bits[e->cur];
     *pitch = e->pitch;
     return GOL_OK;

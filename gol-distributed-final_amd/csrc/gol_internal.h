@@ -9,6 +9,9 @@
 
 #include "golhip.h"
 
+struct gol_comm;
+class gol_ipc;
+
 // Library defaults for the bit-board step (chosen from the gfx950 sweep recorded
 // in DESIGN.md; overridable per engine through gol_config).
 #define GOL_DEFAULT_K 8        // standard layout
@@ -24,9 +27,9 @@
 // so the kernels address input row y as board + y*pitch for -k <= y < R + k.
 #define GOL_GHOST_ROWS 16
 
-// Steps (rounds) of one persistent multi-round launch at most (a launch of the 2^17 x 2^20 board
-// runs ~12 ms per round).
-#define GOL_PERSIST_MAX_ROUNDS 64
+// Device scratch words for the ranks' collectives, pinned host words per shard.
+#define GOL_COLL_WORDS 16
+#define GOL_HOST_WORDS 16
 
 // Timing events per shard before the recorded steps are folded into running sums.
 #define GOL_TIMING_EVENTS 512
@@ -52,17 +55,12 @@ struct gol_shard {
     int64_t counts_cap = 0;
     uint32_t *flag = nullptr;         // nonbinary flag of a load
     uint32_t *err = nullptr;          // device error word of this shard's launches
-    uint32_t *host_word = nullptr;    // pinned readback of err / flag
+    uint32_t *coll = nullptr;         // GOL_COLL_WORDS device words for collectives (agreement, barriers)
+    uint32_t *host_word = nullptr;    // GOL_HOST_WORDS pinned words: readback of err / flag, collectives
     uint8_t *staging = nullptr;       // device byte rows for chunked copies
     uint8_t *host_staging = nullptr;  // pinned host rows
     int64_t stage_rows = 0;
     ncclComm_t nccl = nullptr;
-    // persistent multi-round launches (gol_kernels.h golk_band_persist): claim / done words and
-    // the count slot arrays of one launch
-    uint32_t *pctl = nullptr;
-    int64_t pctl_words = 0;
-    uint64_t *pslots = nullptr;
-    int64_t pslots_n = 0;
     // timing (gol_engine_set_timing): events on `stream` around the timed launches
     std::vector<hipEvent_t> tev;
     size_t tused = 0;
@@ -78,7 +76,7 @@ struct gol_timed {
     int shard;
     size_t ev;  // index of the start event in the shard's pool (stop = ev + 1)
     double cell_updates;
-    int64_t steps;  // k-turn steps between the two events (a persistent launch runs many)
+    int64_t steps;  // k-turn steps between the two events
 };
 
 struct gol_engine {
@@ -91,6 +89,10 @@ struct gol_engine {
     int rank = 0;        // global rank of sh[0] (local shards are consecutive ranks)
     bool rank_mode = false;  // other ranks live in other processes
     int transport = GOL_TRANSPORT_LOCAL;
+    gol_comm *comm = nullptr;  // rank mode: the collectives (RCCL, or the IPC transport's host segment)
+    gol_ipc *ipc = nullptr;    // GOL_TRANSPORT_IPC: the neighbours' mapped buffers and flags (== comm)
+    std::vector<int> ipc_peers;  // global ranks this rank pulls its halo from (itself excluded)
+    uint32_t xn = 0;           // halo exchanges issued (IPC sequence numbers; equal on every rank)
     int64_t min_rows = 0;    // rows of the smallest shard (the broker split: H / nranks)
     bool bit_capable = false;  // W % 64 == 0
     bool band_capable = false; // step the bit board in the band layout
@@ -105,7 +107,6 @@ struct gol_engine {
     int strip = 0;
     int kx = 1;                // halo rows of every exchange (>= the k of any step; gol_step_plan)
     int step_flags = 0;        // GOL_STEP_SERIAL
-    bool persist = false;      // one shard, band k = 12: many steps per launch (GOL_STEP_PERSIST)
     bool halo_ok = false;      // the ghost rows of bits[cur] hold the current halo (kx rows)
     bool halo_issued = false;  // an exchange was enqueued since the last synchronisation point
     bool timing = false;

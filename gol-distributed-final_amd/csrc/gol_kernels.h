@@ -9,12 +9,15 @@
 
 // Flags of a launch's device error word (ORed by the failing waves).
 #define GOLK_ERR_SPIN 1u  // a pipeline wave gave up waiting for an LDS flag (protocol fault)
+#define GOLK_ERR_IPC 2u   // an IPC rank gave up waiting for a neighbour's flag (gol_comm.h)
 
 // Per-device error word for launches made without one (lazily allocated, zeroed).
 uint32_t *golk_device_err_word(int device);
 // Per-device CU slot masks of the band pipeline's role placement (indexed by XCC, SE, SH, CU).
 #define GOL_CU_SLOT_WORDS 2048
 uint32_t *golk_cu_slots(int device);
+// Zero them again on `s` (after a faulted launch whose workgroups may not have freed their slots).
+hipError_t golk_reset_cu_slots(int device, hipStream_t s);
 // Paired-rank claim counters (one buffer per launch stream, gol_kernels.hip StripMap).
 // golk_reset_claims: zero the buffer of stream s, ordered on s (after a faulted launch).
 // golk_release_claims: free it (the caller has synchronised s; an engine destroying its streams).
@@ -40,17 +43,6 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
                           uint64_t *slots, uint32_t *err, hipStream_t s);
 int golk_band_useful_words(int k, int dw);
-// Persistent multi-round band pipeline: `rounds` k = 12 steps of one shard that is the whole
-// torus (rows wrap inside the shard, no ghost rows) in one launch; round r reads buf[r & 1] of
-// (cur, other) and writes the other one, so the result is in cur when rounds is even.  Tiles of
-// `strip` rows (0 = automatic) x one column group.  count_every > 0: the alive count after every
-// count_every-th round into slot array i = (r + 1) / count_every - 1 of `slots` (zeroed by the
-// caller).  ctl: golk_persist_ctl_words(ngroups * nstrips) words, zeroed here on s.
-// golk_persist_geom: false when the board does not fit the tiling (the caller steps per launch).
-bool golk_persist_geom(int64_t R, int64_t Wd, int strip_req, int32_t *strip, int32_t *ngroups, int32_t *nstrips);
-int64_t golk_persist_ctl_words(int64_t tiles);
-hipError_t golk_band_persist(uint32_t *cur, uint32_t *other, int64_t R, int64_t Wd, int64_t pitch, int rounds, int strip,
-                             int count_every, uint32_t *ctl, uint64_t *slots, uint32_t *err, hipStream_t s);
 // Rounds of resident workgroups a step launch over `rows` rows makes (the band pipeline; other
 // kernels: 1e9, i.e. many); for the engine's choice of step plan.
 double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int strip);
@@ -85,3 +77,12 @@ hipError_t golk_row_counts(bool bits_mode, const void *board, const void *prev, 
                            int64_t pitch, int64_t *out, hipStream_t s);
 hipError_t golk_alive_list(bool bits_mode, const void *board, const void *prev, int64_t rows, int64_t width_units,
                            int64_t pitch, const int64_t *offs, int32_t *xy, int64_t cap, int64_t y0, hipStream_t s);
+
+// IPC transport (gol_comm.h): set *flag = value with release ordering at system scope after the
+// stream's earlier work; wait (one wave on the stream) until every flags[i] (i < n <= 4, other
+// processes' flag words mapped through IPC) has reached `want` (wrap-safe sequence compare),
+// then acquire; after timeout_ticks of s_memrealtime (100 MHz) without it, OR GOLK_ERR_IPC into err.
+#define GOLK_IPC_MAX_WAIT 4
+hipError_t golk_ipc_signal(uint32_t *flag, uint32_t value, hipStream_t s);
+hipError_t golk_ipc_wait(const uint32_t *const *flags, int n, uint32_t want, uint64_t timeout_ticks, uint32_t *err,
+                         hipStream_t s);

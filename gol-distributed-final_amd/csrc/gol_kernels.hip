@@ -703,9 +703,6 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 // (work_item).
 // COUNT: the last wave adds the alive cells of the rows it stores to a.slots (branch-free: a
 // per-row uniform mask, no branch around the count as a null-slots check made it).
-// NPIPE > 1 (measurement build, GOL_BAND_NPIPE): one workgroup of NPIPE x P waves per CU holds
-// NPIPE pipelines, each on ONE SIMD (pipeline = the SIMD of its waves from HW_ID, stage = the
-// wave's rank there), so a SIMD serves the stages of a single pipeline.
 // ROWF: hand-off flags count rows instead of 3-row blocks, so a reader may read a row as soon as
 // it is written (one-round launches: +1.2 % on 65536^2; the weak board measured -0.4 % and keeps
 // block flags).
@@ -744,21 +741,11 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
 #ifndef GOL_BAND_LOAD_AUX
 #define GOL_BAND_LOAD_AUX 0
 #endif
-// Measurement builds: issue priority per pipeline role (loader, middle, storer), 0 = none set.
-#ifndef GOL_BAND_ROLE_PRIO
-#define GOL_BAND_ROLE_PRIO 0, 0, 0
-#endif
-// Skip the rule on each wave's fill blocks (0: measurement builds compute them).
-#ifndef GOL_BAND_FILLSKIP
-#define GOL_BAND_FILLSKIP 1
-#endif
-// Pipeline shape of k = 12 (measurement builds may change it): KW stages in each of P waves.
-#ifndef GOL_BAND_KW
+// Pipeline shape of k = 12: KW stages in each of P waves.
 #define GOL_BAND_KW 3
 #define GOL_BAND_P 4
-#endif
-template <int KW, int P, bool CONTIG, bool COUNT, int NPIPE = 1, bool ROWF = false>
-__global__ void __launch_bounds__(64 * P * NPIPE)
+template <int KW, int P, bool CONTIG, bool COUNT, bool ROWF = false>
+__global__ void __launch_bounds__(64 * P)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
 band_pipe_kernel(BitsArgs a)
 {
@@ -768,31 +755,14 @@ band_pipe_kernel(BitsArgs a)
     constexpr int U = band_useful_words(K, DW);
     constexpr int ROW = 64 * DW;
     constexpr int NS = 3;  // (the loops below are unrolled over the 3 slots)
-    __shared__ uint32_t in_ring_[NPIPE][NS][3][ROW];
-    __shared__ uint32_t ring_[NPIPE][P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
-    __shared__ int ready_[NPIPE][P], consumed_[NPIPE][P];
+    __shared__ uint32_t in_ring[NS][3][ROW];
+    __shared__ uint32_t ring_[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
+    __shared__ int ready_[P], consumed_[P];
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (never read; all waves share it)
-    __shared__ int simd_of[NPIPE > 1 ? NPIPE * P : 1];
     __shared__ int place_[P + 2];  // GOL_BAND_PLACE: SIMD of each wave, the CU slot, the mask index
 
     const int lane = threadIdx.x & 63;
-    int pipe = 0, stage = 0;
-    if constexpr (NPIPE > 1) {
-        const int wave = threadIdx.x >> 6;
-        const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u);
-        if (lane == 0) simd_of[wave] = simd;
-        __syncthreads();
-        int r = 0, cnt[4] = {0, 0, 0, 0};
-        for (int i = 0; i < NPIPE * P; ++i) {
-            const int si = simd_of[i];
-            r += (i < wave) & (si == simd);
-            cnt[si & 3] += 1;
-        }
-        const bool even = NPIPE == 4 && cnt[0] == P && cnt[1] == P && cnt[2] == P && cnt[3] == P;
-        pipe = __builtin_amdgcn_readfirstlane(even ? simd : wave % NPIPE);
-        stage = __builtin_amdgcn_readfirstlane(even ? r : wave / NPIPE);
-    }
-    const int litem = NPIPE > 1 ? (int)blockIdx.x * NPIPE + pipe : (int)blockIdx.x;
+    const int litem = (int)blockIdx.x;
     int group, s0, s1, rotv;
     const bool has_rows = work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, litem, group, s0, s1, rotv);
     uint32_t *ctr;
@@ -800,9 +770,8 @@ band_pipe_kernel(BitsArgs a)
     // Pipeline position of this wave, rotated per workgroup: the waves of a workgroup sit on the
     // CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put its
     // loader (global_load_lds) on one SIMD and its storer on another.
-    int wv = NPIPE > 1 ? stage : __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
-    uint32_t (*const in_ring)[3][ROW] = in_ring_[pipe];
-    constexpr bool PLACE = GOL_BAND_PLACE && NPIPE == 1 && P == 4;
+    int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
+    constexpr bool PLACE = GOL_BAND_PLACE && P == 4;
 
     const int64_t col_raw = (int64_t)group * U + (int64_t)(lane - HL) * DW;
     const int64_t band_q = col_raw >= 0 ? col_raw / a.Wd : -((-col_raw + a.Wd - 1) / a.Wd);
@@ -840,16 +809,12 @@ band_pipe_kernel(BitsArgs a)
             y = y > last_in ? last_in : (y < first_in ? first_in : y);
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
-#ifndef GOL_EXP_NOLOAD  // (measurement builds only: -DGOL_EXP_NOLOAD drops the loads, results are garbage)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, GOL_BAND_LOAD_AUX);
-#else
-            (void)g;
-#endif
         }
     };
 
-    if (NPIPE == 1 && !has_rows) return;  // whole workgroup (no barrier after this point)
-    if (threadIdx.x < NPIPE * P) { ready_[threadIdx.x / P][threadIdx.x % P] = 0; consumed_[threadIdx.x / P][threadIdx.x % P] = 0; }
+    if (!has_rows) return;  // whole workgroup (no barrier after this point)
+    if (threadIdx.x < P) { ready_[threadIdx.x] = 0; consumed_[threadIdx.x] = 0; }
     if constexpr (PLACE) {
         if (lane == 0) place_[threadIdx.x >> 6] = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u);
         if (threadIdx.x == 0) {
@@ -859,16 +824,15 @@ band_pipe_kernel(BitsArgs a)
         }
     }
     __syncthreads();
-    if (!has_rows) return;  // a pipeline without rows (no barrier after this point)
     if constexpr (PLACE) {
         const int q = place_[P];
         const int m = (1 << place_[0]) | (1 << place_[1]) | (1 << place_[2]) | (1 << place_[3]);
         if (q >= 0 && m == 0xF) wv = __builtin_amdgcn_readfirstlane((place_[threadIdx.x >> 6] + q) & 3);
     }
-    lds_u32 *const ring_l = (lds_u32 *)&ring_[pipe][0][0][0][0];
-    lds_u32 *const in_l = (lds_u32 *)&in_ring_[pipe][0][0][0];
-    lds_u32 *const ready_l = (lds_u32 *)&ready_[pipe][0];
-    lds_u32 *const consumed_l = (lds_u32 *)&consumed_[pipe][0];
+    lds_u32 *const ring_l = (lds_u32 *)&ring_[0][0][0][0];
+    lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0];
+    lds_u32 *const ready_l = (lds_u32 *)&ready_[0];
+    lds_u32 *const consumed_l = (lds_u32 *)&consumed_[0];
     constexpr int SLOT = 3 * ROW;  // uint32 per slot (one block)
 
     Pipe<KW, DW> p;
@@ -926,9 +890,7 @@ band_pipe_kernel(BitsArgs a)
     uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch_b;
     const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch_b;
     auto emit = [&](const uint32_t (&cur)[DW]) {
-#ifndef GOL_EXP_NOSTORE  // (measurement builds only: -DGOL_EXP_NOSTORE drops the stores)
         __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, GOL_BAND_STORE_AUX);
-#endif
         // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are masked
         // once at the end)
         if constexpr (COUNT) {
@@ -1061,7 +1023,7 @@ band_pipe_kernel(BitsArgs a)
         // own (a branch per block inside the main loop made the compiler spill).  Launches of
         // many rounds only: same box, weak +0.5 %, 262144² +0.7 %, but the one-round ROWF
         // launch (65536²) -2 % (profiles/r03/r03r_ab_fill.jsonl).
-        if constexpr (ROLE != 0 && GOL_BAND_FILLSKIP && !ROWF) {
+        if constexpr (ROLE != 0 && !ROWF) {
             const int nskip = (2 * KW * wv) / 3;
             for (; b + 3 <= nskip; b += 3) {
                 if (!more) break;
@@ -1096,15 +1058,6 @@ band_pipe_kernel(BitsArgs a)
     auto run_role = [&](auto role_c) -> bool {
         return dir ? run(role_c, std::true_type()) : run(role_c, std::false_type());
     };
-    {
-        constexpr int prio[3] = {GOL_BAND_ROLE_PRIO};
-        if constexpr ((prio[0] | prio[1] | prio[2]) != 0) {
-            const int pr = wv == 0 ? prio[0] : (wv == P - 1 ? prio[2] : prio[1]);
-            if (pr == 1) __builtin_amdgcn_s_setprio(1);
-            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-            else if (pr == 3) __builtin_amdgcn_s_setprio(3);
-        }
-    }
     bool ok;
     if (wv == 0) ok = run_role(std::integral_constant<int, 0>());
     else if (wv == P - 1) ok = run_role(std::integral_constant<int, 2>());
@@ -1116,512 +1069,6 @@ band_pipe_kernel(BitsArgs a)
     if constexpr (PLACE) {  // the last wave of the pipeline frees the workgroup's CU slot
         if (wv == P - 1 && lane == 0 && place_[P] >= 0) atomicAnd(a.cu_slots + place_[P + 1], ~(1u << place_[P]));
     }
-}
-
-// ------------------------------------------------------------------ band layout, persistent multi-round pipeline
-// Many k = 12 steps of ONE shard that is the whole torus in one launch.  A step ("round") is cut
-// into tiles (strip of rows x column group, the work item of band_pipe_kernel); tile x of round r
-// reads buf[r & 1] and writes buf[(r + 1) & 1].  Workgroups stay resident and claim tiles in
-// (round, strip, group) order from one counter; before a workgroup loads the rows of tile (r, i,
-// j) it waits until the 3 x 3 tiles around (i, j) (torus) have finished round r - 1: they wrote
-// every row and column it reads (strips >= k rows, column groups >= k words), and they finished
-// reading the buffer it is about to write.  A neighbour can be at most one round ahead, so two
-// buffers suffice.  Every dependency points to an earlier claim, so the claims complete in order
-// whatever the residency (no grid barrier, no deadlock).
-// What it saves against one launch per step (band_pipe_kernel): the kernel boundary and the
-// drain of the last round of workgroups at every step -- a CU starts its next tile while its
-// neighbours finish -- and the pipeline is never drained between the tiles of one workgroup: the
-// loader streams the next tile's rows into the same rings behind the current tile's, so the
-// middle waves see one stream of blocks (a new tile's first 2k outputs mix rows of the old tile
-// and are never stored, as the fill rows of any strip).
-// Hand-off between workgroups (cdna_hip_programming.md Guideline 16, R1): the storer writes its
-// rows write-through (sc1), drains them (s_waitcnt vmcnt(0)), then stores the tile's done count
-// with one sc1 store of lane 0; the loader polls the 9 done words with sc1 loads (one lane each),
-// then acquires (buffer_inv sc1) before the tile's first global_load_lds.  The done word is
-// stored one loop trip into the storer's next tile, whose first 2k rows store nothing: the
-// drain then costs no wait.  Control words (claims, done counts) are zeroed before every launch.
-struct PersistArgs {
-    uint32_t *buf0, *buf1;  // row 0 of the two buffers; round r reads buf[r & 1]
-    int64_t R, Wd, pitch;
-    int32_t rounds, ngroups, nstrips, strip;
-    int32_t count_every;    // fused count after every count_every-th round into slot array (r + 1) / count_every - 1
-    uint32_t div_tiles[2], div_groups[2], div_count[2];  // (magic, shift): n / T, n / ngroups, n / count_every
-    uint32_t *ctl;          // [0] claim counter, [GOL_PERSIST_DONE0 + tile] rounds done (zeroed before the launch)
-    uint64_t *slots;        // count_every > 0: the slot arrays (GOL_COUNT_SLOTS * 8 uint64 each, zeroed)
-    uint32_t *err;
-    uint32_t *cu_slots;
-};
-#define GOL_PERSIST_DONE0 16
-typedef __attribute__((address_space(1))) uint32_t gu32;
-// The lane id, computed where it is used (volatile: not hoisted into a register live across a loop).
-__device__ __forceinline__ int lane_now()
-{
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-// n / d for 0 <= n < 2^31 by a magic multiplier (m, l) from the host (golk_fastdiv): the kernel's
-// few divisions stay on the scalar unit instead of a float reciprocal kept live in VGPRs.
-__device__ __forceinline__ int fdiv(int n, const uint32_t (&d)[2])
-{
-    return (int)((__umulhi((uint32_t)n, d[0]) + (uint32_t)n) >> d[1]);
-}
-
-template <bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
-band_persist_pipe_kernel(PersistArgs a)
-{
-    constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P, DW = 4, K = KW * P;
-    static_assert(P == 4, "four waves: one of every role per SIMD");
-    constexpr int HL = band_halo_lanes(K, DW);
-    constexpr int U = band_useful_words(K, DW);
-    constexpr int ROW = 64 * DW;
-    constexpr int NS = 3;
-    constexpr int SLOT = 3 * ROW;
-    constexpr int SB = SLOT * 4, RB = ROW * 4;
-    constexpr int FINAL = 1 << 30;
-    __shared__ uint32_t in_ring[NS][3][ROW];
-    __shared__ uint32_t ring_[P - 1][NS][3][ROW];
-    __shared__ int ready_[P], consumed_[P];
-    __shared__ int flag_scratch[64];
-    __shared__ int place_[P + 2];
-    __shared__ int tq_[4];    // claimed tiles in stream order, loader -> storer (entry n & 3)
-    __shared__ int text_[4];  // 1: tile n gets a padding trip (the storer signals it at once)
-
-    const int lane = threadIdx.x & 63;
-    const int T = a.nstrips * a.ngroups;
-    const int total = a.rounds * T;
-    if (threadIdx.x < P) { ready_[threadIdx.x] = 0; consumed_[threadIdx.x] = 0; }
-    if (lane == 0) place_[threadIdx.x >> 6] = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u);
-    if (threadIdx.x == 0) {
-        const int t0 = (int)atomicAdd(a.ctl, 1u);
-        tq_[0] = t0;
-        const uint32_t idx = cu_slot_index();
-        place_[P] = (t0 < total && a.cu_slots) ? claim_cu_slot(a.cu_slots + idx) : -1;
-        place_[P + 1] = (int)idx;
-    }
-    __syncthreads();
-    const int tile0 = __builtin_amdgcn_readfirstlane(tq_[0]);
-    if (tile0 >= total) return;  // (no CU slot was claimed)
-    int wv = __builtin_amdgcn_readfirstlane(((int)(threadIdx.x >> 6) + (int)blockIdx.x) % P);
-    {
-        const int q = place_[P];
-        const int m = (1 << place_[0]) | (1 << place_[1]) | (1 << place_[2]) | (1 << place_[3]);
-        if (q >= 0 && m == 0xF) wv = __builtin_amdgcn_readfirstlane((place_[threadIdx.x >> 6] + q) & 3);
-    }
-
-    const int R = (int)a.R, Wd = (int)a.Wd;
-    const int pitch_b = (int)a.pitch * 4;
-    // tile t: round r, strip [s0, s1), column group, blocks of its stream (a multiple of 3)
-    // (every value wave-uniform: scalar registers)
-    auto geom = [&](int t, int &r, int &s0, int &s1, int &group, int &nb3) {
-        r = __builtin_amdgcn_readfirstlane(fdiv(t, a.div_tiles));
-        const int x = t - r * T;
-        const int si = __builtin_amdgcn_readfirstlane(fdiv(x, a.div_groups));
-        group = __builtin_amdgcn_readfirstlane(x - si * a.ngroups);
-        s0 = si * a.strip;
-        s1 = si == a.nstrips - 1 ? R : s0 + a.strip;  // the last strip takes the remainder
-        nb3 = __builtin_amdgcn_readfirstlane(((s1 - s0 + 2 * K + 2) / 3 + 2) / 3 * 3);
-    };
-    auto buf_of = [&](int r) {  // (a scalar select: both pointers are kernel arguments)
-        const uint64_t p = (r & 1) ? (uint64_t)a.buf1 : (uint64_t)a.buf0;
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-        return reinterpret_cast<char *>(((uint64_t)hi << 32) | lo);
-    };
-    // this lane's words of a column group (band_pipe_kernel)
-    auto cols = [&](int group, uint32_t &lane_off, uint32_t &rot, bool &wrap, bool &writer) {
-        const int lane = lane_now();  // (not kept live across the loops: registers are at their limit)
-        const int col_raw = group * U + (lane - HL) * DW;
-        const int q = col_raw < 0 ? -1 : (col_raw >= Wd ? 1 : 0);  // Wd >= 256: one band at most either way
-        lane_off = (uint32_t)(col_raw - q * Wd) * 4u;
-        rot = (uint32_t)q & 31u;
-        wrap = __ballot(rot != 0) != 0;
-        writer = lane >= HL && lane < 64 - HL && col_raw < Wd;
-    };
-
-    lds_u32 *const ring_l = (lds_u32 *)&ring_[0][0][0][0];
-    lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0];
-    lds_u32 *const ready_l = (lds_u32 *)&ready_[0];
-    lds_u32 *const consumed_l = (lds_u32 *)&consumed_[0];
-    lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
-    lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;
-    lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;
-    lds_u32 *const in_base = in_l + lane * 4;
-    lds_u32 *const rd_base = ring_l + (wv - 1) * NS * SLOT + lane * 4;
-    lds_u32 *const wr_base = ring_l + wv * NS * SLOT + lane * 4;
-    lds_u32 *const src_base = wv == 0 ? in_base : rd_base;
-
-    Pipe<KW, DW> p;
-    pipe_init(p);
-    int seen_ready = 0, seen_free = 0;
-    bool ok = true, more = true;  // ok: no wait of this wave timed out
-#ifdef GOL_PERSIST_STATS  // measurement builds: wait times per role (s_memrealtime, 100 MHz) into ctl[1..15]
-    uint64_t st_wait = 0, st_dep = 0;
-    const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
-#define GOL_TIMED(acc, expr) ({ const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); auto r_ = (expr); acc += __builtin_amdgcn_s_memrealtime() - t_; r_; })
-#else
-#define GOL_TIMED(acc, expr) (expr)
-#endif
-
-    // ---- loader state: the tile whose rows it computes (realignment) and the tile it loads
-    int c_r, c_s0, c_s1, c_group, c_nb3;
-    geom(tile0, c_r, c_s0, c_s1, c_group, c_nb3);
-    uint32_t c_off, c_rot;
-    bool c_wrap, c_writer;
-    cols(c_group, c_off, c_rot, c_wrap, c_writer);
-    const char *ld_src = buf_of(c_r);
-    int ld_first = c_s0 - K, ld_last = c_s1 + K - 1, ld_base = 0;
-    uint32_t ld_off = c_off;
-    // wave 0: stream block gb of the tile being loaded -> in_ring slot (rows wrap around the torus)
-    auto stage_in = [&](int gb, uint32_t (*slot)[ROW]) {
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            int y = ld_first + 3 * (gb - ld_base) + s;
-            y = y > ld_last ? ld_last : y;
-            y += y < 0 ? R : 0;
-            y -= y >= R ? R : 0;
-            const char *g = ld_src + (int64_t)y * pitch_b + ld_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, 0);
-        }
-    };
-    // wave 0: have the 3 x 3 tiles around tile t done round r - 1?  Lane i < 9 polls neighbour
-    // (i / 3 - 1, i % 3 - 1) with an sc1 load; `polls` bounded, then false.  After a match the
-    // caller acquires (the neighbours' rows are stored write-through: drop this CU's stale copies).
-    auto deps_done = [&](int t, int polls) -> bool {
-        int r, s0, s1, group, nb3;
-        geom(t, r, s0, s1, group, nb3);
-        if (r == 0) return true;  // round 0 reads what earlier launches wrote
-        int ni = fdiv(t - r * T, a.div_groups) + lane / 3 - 1, nj = group + lane % 3 - 1;
-        ni += ni < 0 ? a.nstrips : 0;
-        ni -= ni >= a.nstrips ? a.nstrips : 0;
-        nj += nj < 0 ? a.ngroups : 0;
-        nj -= nj >= a.ngroups ? a.ngroups : 0;
-        gu32 *f = (gu32 *)(a.ctl + GOL_PERSIST_DONE0) + (lane < 9 ? ni * a.ngroups + nj : 0);
-#pragma clang loop unroll(disable)
-        for (int n = 0; n < polls; ++n) {
-            const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__ballot(lane < 9 && v < (uint32_t)r) == 0) return true;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        return false;
-    };
-    auto acquire = [&]() { asm volatile("buffer_inv sc1" ::: "memory"); };
-
-    // ---- storer state: the tile whose rows it stores
-    const uint32_t nrows0 = (uint32_t)(c_s1 - c_s0);
-    uint32_t nrows = nrows0;
-    // the row store offset; halo lanes store outside the buffer (from 2^31 on).  The lane's
-    // column offset is voff - rrel * pitch (no register of its own).
-    const uint32_t st_off0 = c_writer ? c_off : 0x80000000u;
-    __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
-        buf_of(c_r + 1) + (int64_t)c_s0 * pitch_b, (short)0, (int)(nrows * (uint32_t)pitch_b), 0x00020000);
-    int rrel = -2 * K;
-    uint32_t voff = st_off0 + (uint32_t)rrel * (uint32_t)pitch_b;
-    uint32_t alive = 0;
-    auto unpack = [&](const v4u32 v, uint32_t (&cur)[DW]) { cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w; };
-    auto pack = [&](const uint32_t (&cur)[DW]) { return v4u32{cur[0], cur[1], cur[2], cur[3]}; };
-    auto compute = [&](auto s_c, uint32_t (&cur)[DW]) {
-        constexpr int S = decltype(s_c)::value;
-#pragma unroll
-        for (int g = 0; g < KW; ++g) bstage_seq<KW, DW, S>(p, g, cur);
-    };
-    // A wait that times out clears `ok` and the wave runs on without waiting to the end of its
-    // loop trip (no exit inside a trip: the compiler would merge the in-flight row register
-    // with a copy on the exit path).
-    auto publish_and_reserve = [&](int b) {
-        lds_wait1();
-        lds_flag_wr(rdy_addr, b);
-        if (ok && seen_free < b + 1 - NS) {
-            seen_free = GOL_TIMED(st_wait, spin_until_ge(consumed_l + wv + 1, b + 1 - NS));
-            if (seen_free < 0) ok = false;
-        }
-    };
-    auto emit = [&](const uint32_t (&cur)[DW]) {
-        __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, 16 /* sc1: write-through */);
-        if constexpr (COUNT) {
-            // (volatile: counted here, so the row's registers are free after its store; a count the
-            // compiler sank to the end of the trip kept three rows live and spilled)
-            uint32_t c;
-            asm volatile("v_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0\n\tv_bcnt_u32_b32 %0, %3, %0\n\t"
-                         "v_bcnt_u32_b32 %0, %4, %0"
-                         : "=&v"(c) : "v"(cur[0]), "v"(cur[1]), "v"(cur[2]), "v"(cur[3]));
-            alive += (uint32_t)rrel < nrows ? c : 0u;
-        }
-        voff += (uint32_t)pitch_b;
-        rrel += 1;
-    };
-
-    uint32_t pending = 0;   // loader: the claim in flight (the tile after the current one)
-    bool claimed = false;   // loader: the claim was issued in this loop trip (one more VMEM op in flight)
-    // The first tile may belong to a later round (a workgroup that started late): nothing is in
-    // this pipeline yet, so the loader may simply wait.
-    if (wv == 0) {
-        if (GOL_TIMED(st_dep, deps_done(tile0, GOL_SPIN_LIMIT))) {
-            acquire();
-            stage_in(0, in_ring[0]);
-            stage_in(1, in_ring[1]);
-            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        } else {
-            ok = more = false;
-            lds_flag_wr(rdy_addr, FINAL);  // the pipeline ends before its first block
-        }
-    } else if (seen_ready < 1) {
-        seen_ready = spin_until_ge(ready_l + wv, 1);
-        if (seen_ready < 0) ok = more = false;
-        else more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
-    }
-    v4u32 nextv{0, 0, 0, 0};
-    if (more) {
-        nextv = lds_rd128(src_base);
-        lds_flag_wr(wv == 0 ? scratch : cns_addr, 0);
-    }
-
-    auto step = [&](int b, auto u_c, auto role_c) {
-        constexpr int US = decltype(u_c)::value;
-        constexpr int ROLE = decltype(role_c)::value;
-        constexpr bool LAST = ROLE == 2;
-        uint32_t cur[DW];
-        auto realign = [&]() {
-            if (ROLE == 0 && c_wrap) {
-#pragma unroll
-                for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], c_rot);
-            }
-        };
-        // row 0
-        lds_wait_n<1>(nextv);
-        unpack(nextv, cur);
-        nextv = lds_rd128_issue_o<US * SB + RB>(src_base);
-        realign();
-        compute(std::integral_constant<int, 0>(), cur);
-        if constexpr (LAST) {
-            emit(cur);
-        } else {
-            publish_and_reserve(b);
-            lds_wr128_o<US * SB>(wr_base, pack(cur));
-        }
-        // row 1
-        lds_wait_n<LAST ? 0 : 1>(nextv);
-        unpack(nextv, cur);
-        nextv = lds_rd128_issue_o<US * SB + 2 * RB>(src_base);
-        realign();
-        compute(std::integral_constant<int, 1>(), cur);
-        if constexpr (LAST) emit(cur);
-        else lds_wr128_o<US * SB + RB>(wr_base, pack(cur));
-        // row 2; row 0 of block b+1 is read during it
-        lds_wait_n<LAST ? 0 : 1>(nextv);
-        unpack(nextv, cur);
-        if constexpr (ROLE == 0) {
-            stage_in(b + 2, in_ring[(US + 2) % 3]);
-            // block b+1 landed, b+2 in flight (and at US 1 the claim issued at US 0)
-            if (US == 1 && claimed) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            if constexpr (US == 0) {
-                if (claimed && lane == 0) pending = atomicAdd(a.ctl, 1u);
-            }
-            nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
-            lds_flag_wr(scratch, 0);
-        } else {
-            if (ok && seen_ready < b + 2) {
-                seen_ready = GOL_TIMED(st_wait, spin_until_ge(ready_l + wv, b + 2));
-                if (seen_ready < 0) ok = false;
-            }
-            more = ok && (seen_ready < FINAL || b + 1 < seen_ready - FINAL);
-            // (read even after the last block: a conditional read would make the compiler merge
-            // the in-flight register with the old value by a copy)
-            nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
-            lds_flag_wr(cns_addr, b + 1);
-        }
-        realign();
-        compute(std::integral_constant<int, 2>(), cur);
-        if constexpr (LAST) emit(cur);
-        else lds_wr128_o<US * SB + 2 * RB>(wr_base, pack(cur));
-    };
-
-    // Tile hand-over inside the pipeline.  At the start of a tile's last loop trip the loader
-    // reads its next claim and polls that tile's neighbours once.
-    //  * Done (the usual case): it acquires and loads the next tile's first two blocks during this
-    //    trip, right behind this tile's last block; the storer signals this tile one trip into the
-    //    next one (its first 2k rows store nothing, so the drain costs no wait).
-    //  * Not done: waiting now could deadlock -- the next tile may depend (also through other
-    //    workgroups) on THIS tile, which completes only once this pipeline has stored it.  A wave
-    //    finishes block b only once its producer has published block b+1, so the storer finishes
-    //    the tile's last block L once the loader has published L+3: the tile gets one padding trip
-    //    (blocks L+1..L+3: clamped rows, stores outside the strip), the loader computes it and
-    //    publishes it, and only then waits; the storer stores L and signals the tile at once
-    //    (text_ tells it so).  After the wait the loader loads the next tile's first two blocks.
-    int gb = 0;  // first block of the loop trip
-    if (ok && wv == 0) {
-        int lb = 0, nseq = 0, nt = total;
-        bool pad_trip = false;
-        for (;;) {
-            bool trans = false;  // the load context moves to tile nt after step 0 of this trip
-            bool last_base = false;
-            if (!pad_trip && lb + 3 == c_nb3) {
-                last_base = true;
-                nt = __builtin_amdgcn_readfirstlane((int)pending);
-                int pad = 0;
-                if (nt < total) {
-                    if (deps_done(nt, 1)) {
-                        acquire();  // complete before the next tile's loads: step 0's vmcnt(3) waits for it
-                        trans = true;
-                    } else {
-                        pad = 1;
-                    }
-#ifdef GOL_PERSIST_STATS
-                    if (lane == 0) atomicAdd(a.ctl + (pad ? 1 : 14), 1u);
-#endif
-                }
-                asm volatile("ds_write_b32 %0, %1" ::"v"(lane == 0 ? (lds_u32 *)&text_[nseq & 3] : scratch), "v"(pad)
-                             : "memory");
-                if (trans) {
-                    ++nseq;
-                    asm volatile("ds_write_b32 %0, %1" ::"v"(lane == 0 ? (lds_u32 *)&tq_[nseq & 3] : scratch), "v"(nt)
-                                 : "memory");
-                }
-            }
-            claimed = lb == 0;  // claim the tile after the next during the first trip of a tile
-            int n_r = 0, n_s0 = 0, n_s1 = 0, n_group = 0, n_nb3 = 0;
-            uint32_t n_rot = 0;
-            bool n_wrap = false, n_writer = false;
-            auto to_next = [&]() {  // blocks gb+3 on are tile nt's
-                geom(nt, n_r, n_s0, n_s1, n_group, n_nb3);
-                cols(n_group, ld_off, n_rot, n_wrap, n_writer);
-                ld_src = buf_of(n_r);
-                ld_first = n_s0 - K;
-                ld_last = n_s1 + K - 1;
-                ld_base = gb + 3;
-            };
-            step(gb, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
-            if (trans) to_next();
-            step(gb + 1, std::integral_constant<int, 1>(), std::integral_constant<int, 0>());
-            step(gb + 2, std::integral_constant<int, 2>(), std::integral_constant<int, 0>());
-            lds_settle<2>(nextv);  // younger: the scratch flag write, the row-2 write
-            if (!ok) {
-                gb += 3;
-                break;
-            }
-            if (pad_trip) {
-                // the padding trip is written (its loads of blocks gb+3, gb+4 were clamped rows of this
-                // tile): publish it, wait for tile nt's neighbours, then load nt's first two blocks
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                lds_flag_wr(rdy_addr, gb + 3);
-                if (!GOL_TIMED(st_dep, deps_done(nt, GOL_SPIN_LIMIT))) {
-                    ok = false;
-                    gb += 3;
-                    break;
-                }
-                acquire();
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate, the clamped loads
-                ++nseq;
-                asm volatile("ds_write_b32 %0, %1" ::"v"(lane == 0 ? (lds_u32 *)&tq_[nseq & 3] : scratch), "v"(nt)
-                             : "memory");
-                to_next();
-                stage_in(gb + 3, in_ring[0]);  // (gb + 3 is a multiple of 3: ring slots 0 and 1)
-                stage_in(gb + 4, in_ring[1]);
-                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-                nextv = lds_rd128(src_base);  // row 0 of block gb+3, loaded now
-                lds_flag_wr(scratch, 0);      // (the younger LDS operation step 0's first wait leaves)
-                trans = true;
-            }
-            gb += 3;
-            if (trans) {  // the compute context follows: realignment of tile nt's rows
-                c_rot = n_rot;
-                c_wrap = n_wrap;
-                c_nb3 = n_nb3;
-                lb = 0;
-                pad_trip = false;
-                continue;
-            }
-            if (last_base && nt >= total) break;
-            if (last_base) pad_trip = true;
-            lb += 3;
-        }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        lds_flag_wr(rdy_addr, FINAL + gb);
-    } else if (ok && wv < P - 1) {
-        while (more) {
-            step(gb, std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
-            step(gb + 1, std::integral_constant<int, 1>(), std::integral_constant<int, 1>());
-            step(gb + 2, std::integral_constant<int, 2>(), std::integral_constant<int, 1>());
-            lds_settle<2>(nextv);  // younger: the consumed flag write, the row-2 write
-            gb += 3;
-        }
-        if (ok) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_flag_wr(rdy_addr, FINAL + gb);
-        }
-    } else if (ok) {
-        int lb = 0, sseq = 0;
-        int s_tile = tile0, s_r = c_r, s_nb3 = c_nb3;
-        bool s_pad = false;  // in the tile's padding trip
-        // the tile whose rows are stored but not yet signalled (its position, round)
-        int p_pos = -1, p_r = 0;
-        auto signal = [&]() {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its rows are in memory (sc1 stores)
-            // (every lane stores the same word: no exec mask, no lane id kept live)
-            __hip_atomic_store((gu32 *)(a.ctl + GOL_PERSIST_DONE0) + p_pos, (uint32_t)(p_r + 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            p_pos = -1;
-        };
-        while (more) {
-            if (lb == s_nb3) {  // the next tile (its id was written before its first block was published)
-                ++sseq;
-                s_tile = __builtin_amdgcn_readfirstlane(lds_rd32((const lds_u32 *)&tq_[sseq & 3]));
-                int s0, s1, group;
-                geom(s_tile, s_r, s0, s1, group, s_nb3);
-                uint32_t off, rot;
-                bool wrap, writer;
-                cols(group, off, rot, wrap, writer);
-                nrows = (uint32_t)(s1 - s0);
-                strip_rs = __builtin_amdgcn_make_buffer_rsrc(buf_of(s_r + 1) + (int64_t)s0 * pitch_b, (short)0,
-                                                             (int)(nrows * (uint32_t)pitch_b), 0x00020000);
-                rrel = -2 * K;
-                voff = (writer ? off : 0x80000000u) + (uint32_t)rrel * (uint32_t)pitch_b;
-                lb = 0;
-                s_pad = false;
-            }
-            if (lb == 3 && p_pos >= 0) signal();  // one trip in: the new tile's stores so far were all dropped
-            step(gb, std::integral_constant<int, 0>(), std::integral_constant<int, 2>());
-            step(gb + 1, std::integral_constant<int, 1>(), std::integral_constant<int, 2>());
-            step(gb + 2, std::integral_constant<int, 2>(), std::integral_constant<int, 2>());
-            lds_settle<1>(nextv);  // younger: the consumed flag write
-            gb += 3;
-            lb += 3;
-            if (lb == s_nb3 && !s_pad) {  // the tile's rows are stored
-                p_pos = s_tile - s_r * T;
-                p_r = s_r;
-                if constexpr (COUNT) {  // a count round: every lane adds its rows' count to a slot of its own
-                    const int ci = fdiv(s_r + 1, a.div_count);
-                    if (a.count_every > 0 && ci * a.count_every == s_r + 1) {
-                        // (halo lanes' rows are not this group's)
-                        const uint32_t st_off = voff - (uint32_t)rrel * (uint32_t)pitch_b;
-                        const uint32_t c = alive & (st_off != 0x80000000u ? 0xFFFFFFFFu : 0u);
-                        atomicAdd((unsigned long long *)&a.slots[(int64_t)(ci - 1) * (GOL_COUNT_SLOTS * 8) +
-                                                                 ((blockIdx.x & 3) * 64 + lane_now()) * 8],
-                                  (unsigned long long)c);
-                    }
-                    alive = 0;
-                }
-                if (__builtin_amdgcn_readfirstlane(lds_rd32((const lds_u32 *)&text_[sseq & 3]))) {  // the loader waits: signal now
-                    signal();
-                    s_nb3 += 3;
-                    s_pad = true;
-                }
-            }
-        }
-        if (ok && p_pos >= 0) signal();
-    }
-#ifdef GOL_PERSIST_STATS
-    if (lane == 0) {
-        unsigned long long *q = (unsigned long long *)(a.ctl + 2);  // [0] dep waits (loader), [1..3] flag waits per role, [4] lifetimes
-        atomicAdd(q + 0, (unsigned long long)st_dep);
-        atomicAdd(q + 1 + (wv == 0 ? 0 : (wv == P - 1 ? 2 : 1)), (unsigned long long)st_wait);
-        atomicAdd(q + 4, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - st_t0));
-    }
-#endif
-    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
-    if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (wv == P - 1 && lane == 0 && place_[P] >= 0) atomicAnd(a.cu_slots + place_[P + 1], ~(1u << place_[P]));
 }
 
 // 32 x 32 bit-matrix transpose in registers: afterwards x[i] bit b = (before) x[b] bit i.
@@ -2485,6 +1932,45 @@ __global__ void row_counts_bytes_kernel(const uint8_t *bytes, const uint8_t *pre
 
 }  // namespace golk
 
+// ------------------------------------------------------------------ IPC sequence flags
+// The IPC halo transport (gol_ipc.cpp): a rank's flag words live in its own HBM and are polled by
+// its ring neighbours' kernels through IPC mappings (other processes, the same or another GPU).
+// Stream order puts a signal after the launches whose rows it announces (their end-of-kernel
+// release has written them back), and the copy after the wait that acquired the flag.
+__global__ void ipc_signal_kernel(uint32_t *flag, uint32_t value)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct IpcWaitArgs {
+    const uint32_t *f0, *f1, *f2, *f3;
+    int32_t n;
+    uint32_t want;
+    uint64_t timeout;
+    uint32_t *err;
+};
+
+// Lane i < n polls flag i (a bounded wait: every lane leaves, with or without the flag).
+__global__ void ipc_wait_kernel(IpcWaitArgs a)
+{
+    const int lane = threadIdx.x;
+    bool ok = true;
+    if (lane < a.n) {
+        const uint32_t *f = lane == 0 ? a.f0 : (lane == 1 ? a.f1 : (lane == 2 ? a.f2 : a.f3));
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            const uint32_t v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((int32_t)(v - a.want) >= 0) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    if (!ok) atomicOr(a.err, GOLK_ERR_IPC);
+}
+
 // ------------------------------------------------------------------ launchers
 using namespace golk;
 
@@ -2537,6 +2023,12 @@ uint32_t *golk_cu_slots(int device)
     (void)hipSetDevice(prev);
     if (w) tabs[device] = w;
     return w;
+}
+
+hipError_t golk_reset_cu_slots(int device, hipStream_t s)
+{
+    uint32_t *w = golk_cu_slots(device);
+    return w ? hipMemsetAsync(w, 0, GOL_CU_SLOT_WORDS * sizeof(uint32_t), s) : hipErrorOutOfMemory;
 }
 
 static uint32_t *err_or_default(uint32_t *err)
@@ -2742,17 +2234,27 @@ void golk_own_stream(hipStream_t s)
 
 hipError_t golk_reset_claims_device(int device)
 {
+    // Synchronous, on the null stream between two device-wide synchronisations: a caller's stream
+    // that owns a buffer here may have been destroyed since (its handle is not used), and the
+    // second synchronisation orders the zeroing before any later launch on a non-blocking stream.
     std::lock_guard<std::mutex> lock(claims_mu);
-    int cus = 0;
+    int cus = 0, prev = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    bool any = false;
+    if (e == hipSuccess) e = hipGetDevice(&prev);
+    if (e == hipSuccess) e = hipSetDevice(device);
+    if (e != hipSuccess) return e;
+    e = hipDeviceSynchronize();
     for (auto &kv : claims_bufs) {
         if (e != hipSuccess) break;
         if (kv.first.second != device || engine_streams.count(kv.first.first)) continue;
-        e = hipMemsetAsync(kv.second, 0, claims_bytes(cus), kv.first.first);
-        any = true;
+        e = hipMemset(kv.second, 0, claims_bytes(cus));
     }
-    if (e == hipSuccess && any) e = hipDeviceSynchronize();  // gol_dev_error is synchronous
+    if (e == hipSuccess) {
+        uint32_t *w = golk_cu_slots(device);  // (placement only: a timed-out workgroup kept its slot)
+        if (w) e = hipMemset(w, 0, GOL_CU_SLOT_WORDS * sizeof(uint32_t));
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipSetDevice(prev);
     return e;
 }
 
@@ -2853,27 +2355,10 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 #define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
 static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
 
-#ifndef GOL_BAND_NPIPE
-#define GOL_BAND_NPIPE 1
-#endif
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
     constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
-    if constexpr (GOL_BAND_NPIPE > 1) {  // measurement build: pipelines on one SIMD each
-        constexpr int NP = GOL_BAND_NPIPE;
-        const bool count = a.slots != nullptr;
-        const void *kf = (const void *)band_pipe_kernel<KW, P, true, true, NP>;
-        const int64_t slots = resident_workgroups(kf, 64 * P * NP) * NP;
-        if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
-        const int64_t items = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
-        const dim3 g((unsigned)((items + NP - 1) / NP)), b(64 * P * NP);
-        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, NP>), g, b, 0, s, a);
-        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, NP>), g, b, 0, s, a);
-        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, NP>), g, b, 0, s, a);
-        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, NP>), g, b, 0, s, a);
-        return hipGetLastError();
-    }
     const bool count = a.slots != nullptr;
     const void *kf = contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true> : (const void *)band_pipe_kernel<KW, P, true, false>)
                             : (count ? (const void *)band_pipe_kernel<KW, P, false, true> : (const void *)band_pipe_kernel<KW, P, false, false>);
@@ -2903,10 +2388,10 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
     }
     const dim3 g((unsigned)nwg), blk(64 * P);
     if (a.sm.ranked) {  // one-round launch: row-grain hand-off flags
-        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, 1, true>), g, blk, 0, s, a);
-        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, 1, true>), g, blk, 0, s, a);
-        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, 1, true>), g, blk, 0, s, a);
-        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, 1, true>), g, blk, 0, s, a);
+        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, true>), g, blk, 0, s, a);
+        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, true>), g, blk, 0, s, a);
+        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, true>), g, blk, 0, s, a);
+        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, true>), g, blk, 0, s, a);
     } else if (contig && count) {
         hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), g, blk, 0, s, a);
     } else if (contig) {
@@ -2965,89 +2450,6 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
 }
 
 int golk_band_useful_words(int k, int dw) { return band_useful_words(k, dw); }
-
-// ---- persistent multi-round band pipeline (band_persist_pipe_kernel)
-static constexpr int PERSIST_K = GOL_BAND_KW * GOL_BAND_P;
-
-// (m, l) with n / d == (umulhi(n, m) + n) >> l for 0 <= n < 2^31 (1 <= d < 2^31): l = ceil(log2 d),
-// m = floor(2^32 (2^l - d) / d) + 1 (Granlund & Montgomery; the sum stays below 2^32).
-static void golk_fastdiv(uint32_t d, uint32_t (&out)[2])
-{
-    uint32_t l = 0;
-    while ((uint64_t(1) << l) < d) ++l;
-    out[0] = (uint32_t)(((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1);
-    out[1] = l;
-}
-
-bool golk_persist_geom(int64_t R, int64_t Wd, int strip_req, int32_t *strip, int32_t *ngroups, int32_t *nstrips)
-{
-    const int64_t U = band_useful_words(PERSIST_K, 4);
-    if (R < 3 * PERSIST_K || Wd < 256 || Wd % 4 || Wd > (int64_t(1) << 26) || R > (int64_t(1) << 30)) return false;
-    const int64_t ng = (Wd + U - 1) / U;
-    // a neighbour's halo (k words) must lie within the next column group, the last one included
-    if (ng > 1 && Wd - (ng - 1) * U < PERSIST_K) return false;
-    int64_t st = strip_req;
-    if (st <= 0) {
-        // tiles per round >= ~2x the resident workgroups (a round's tiles then start as their
-        // neighbours of the previous round end), strips of 96 .. 1024 rows (fill rows <= 25 %)
-        const int64_t slots = std::max<int64_t>(
-            1, resident_workgroups((const void *)band_persist_pipe_kernel<true>, 64 * GOL_BAND_P));
-        st = std::min<int64_t>(1024, std::max<int64_t>(96, R * ng / (2 * slots)));
-    }
-    st = std::min(st, R);
-    const int64_t ns = std::max<int64_t>(1, R / st);
-    st = R / ns;  // ns strips of st rows, the last one with the remainder (< ns rows more)
-    const int64_t last = R - (ns - 1) * st;
-    // strips of >= k rows (a neighbour's halo lies in the next strip); one store buffer per strip
-    if (st < PERSIST_K || last * Wd * 4 >= (int64_t(1) << 31) || ng * ns > (int64_t(1) << 24)) return false;
-    *strip = (int32_t)st;
-    *ngroups = (int32_t)ng;
-    *nstrips = (int32_t)ns;
-    return true;
-}
-
-int64_t golk_persist_ctl_words(int64_t tiles) { return (GOL_PERSIST_DONE0 + tiles + 3) / 4 * 4; }
-
-hipError_t golk_band_persist(uint32_t *cur, uint32_t *other, int64_t R, int64_t Wd, int64_t pitch, int rounds, int strip,
-                             int count_every, uint32_t *ctl, uint64_t *slots, uint32_t *err, hipStream_t s)
-{
-    if (rounds <= 0) return hipSuccess;
-    PersistArgs a;
-    a.buf0 = cur;
-    a.buf1 = other;
-    a.R = R;
-    a.Wd = Wd;
-    a.pitch = pitch;
-    a.rounds = rounds;
-    if (!golk_persist_geom(R, Wd, strip, &a.strip, &a.ngroups, &a.nstrips)) return hipErrorInvalidValue;
-    const int64_t tiles = (int64_t)a.ngroups * a.nstrips;
-    if (tiles * rounds >= (int64_t(1) << 31)) return hipErrorInvalidValue;
-    a.count_every = slots ? count_every : 0;
-    golk_fastdiv((uint32_t)tiles, a.div_tiles);
-    golk_fastdiv((uint32_t)a.ngroups, a.div_groups);
-    golk_fastdiv((uint32_t)std::max(1, a.count_every), a.div_count);
-    a.ctl = ctl;
-    a.slots = slots;
-    a.err = err_or_default(err);
-    if (!a.err) return hipErrorOutOfMemory;
-    a.cu_slots = nullptr;
-    if (GOL_BAND_PLACE) {
-        int dev = 0;
-        if (hipGetDevice(&dev) == hipSuccess) a.cu_slots = golk_cu_slots(dev);
-    }
-    // every polled word zeroed before every launch (claims, done counts), on the launch stream
-    hipError_t e = hipMemsetAsync(ctl, 0, golk_persist_ctl_words(tiles) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    const bool count = a.count_every > 0;
-    const void *kf = count ? (const void *)band_persist_pipe_kernel<true> : (const void *)band_persist_pipe_kernel<false>;
-    int64_t nwg = resident_workgroups(kf, 64 * GOL_BAND_P);
-    if (nwg <= 0) nwg = 1024;
-    nwg = std::min<int64_t>(nwg, tiles * rounds);
-    const dim3 g((unsigned)nwg), blk(64 * GOL_BAND_P);
-    if (count) hipLaunchKernelGGL((band_persist_pipe_kernel<true>), g, blk, 0, s, a);
-    else hipLaunchKernelGGL((band_persist_pipe_kernel<false>), g, blk, 0, s, a);
-    return hipGetLastError();
-}
 
 double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int strip)
 {
@@ -3246,5 +2648,29 @@ hipError_t golk_alive_list(bool bits_mode, const void *board, const void *prev, 
     else
         hipLaunchKernelGGL(alive_list_bytes_kernel, grid, dim3(64 * wpb), 0, s, (const uint8_t *)board,
                            (const uint8_t *)prev, rows, width_units, pitch, offs, xy, cap, y0);
+    return hipGetLastError();
+}
+
+hipError_t golk_ipc_signal(uint32_t *flag, uint32_t value, hipStream_t s)
+{
+    hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, s, flag, value);
+    return hipGetLastError();
+}
+
+hipError_t golk_ipc_wait(const uint32_t *const *flags, int n, uint32_t want, uint64_t timeout_ticks, uint32_t *err,
+                         hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    if (n > GOLK_IPC_MAX_WAIT || !err) return hipErrorInvalidValue;
+    IpcWaitArgs a;
+    a.f0 = flags[0];
+    a.f1 = n > 1 ? flags[1] : flags[0];
+    a.f2 = n > 2 ? flags[2] : flags[0];
+    a.f3 = n > 3 ? flags[3] : flags[0];
+    a.n = n;
+    a.want = want;
+    a.timeout = timeout_ticks;
+    a.err = err;
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }

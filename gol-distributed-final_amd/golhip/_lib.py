@@ -23,14 +23,17 @@ GOL_EQUIT = -7
 GOL_ECOMM = -8
 GOL_COUNT_SLOTS = 256
 GOL_RCCL_ID_BYTES = 128
+GOL_IPC_ID_BYTES = 128
+GOL_IPC_MAX_RANKS = 16
 GOL_LAYOUT_AUTO, GOL_LAYOUT_STANDARD, GOL_LAYOUT_BAND = 0, 1, 2
 LAYOUTS = {"auto": GOL_LAYOUT_AUTO, "standard": GOL_LAYOUT_STANDARD, "band": GOL_LAYOUT_BAND}
-GOL_TRANSPORT_AUTO, GOL_TRANSPORT_LOOPBACK, GOL_TRANSPORT_RCCL, GOL_TRANSPORT_LOCAL = 0, 1, 2, 3
-TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "rccl": GOL_TRANSPORT_RCCL}
-TRANSPORT_NAMES = {GOL_TRANSPORT_LOOPBACK: "loopback", GOL_TRANSPORT_RCCL: "rccl", GOL_TRANSPORT_LOCAL: "local"}
+GOL_TRANSPORT_AUTO, GOL_TRANSPORT_LOOPBACK, GOL_TRANSPORT_RCCL, GOL_TRANSPORT_LOCAL, GOL_TRANSPORT_IPC = 0, 1, 2, 3, 4
+TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "rccl": GOL_TRANSPORT_RCCL,
+              "ipc": GOL_TRANSPORT_IPC}
+TRANSPORT_NAMES = {GOL_TRANSPORT_LOOPBACK: "loopback", GOL_TRANSPORT_RCCL: "rccl", GOL_TRANSPORT_LOCAL: "local",
+                   GOL_TRANSPORT_IPC: "ipc"}
 GOL_SHARDS_SAME_DEVICE = 1
 GOL_STEP_SERIAL, GOL_STEP_EDGE_FIRST, GOL_STEP_OVERLAP = 2, 4, 8
-GOL_STEP_PERSIST = 16
 STEP_MODES = {"auto": 0, "serial": GOL_STEP_SERIAL, "edge_first": GOL_STEP_EDGE_FIRST, "overlap": GOL_STEP_OVERLAP}
 GOL_HALO_SEND, GOL_HALO_RECV = 0, 1
 GOL_LAUNCH_MAIN, GOL_LAUNCH_EDGE = 0, 1
@@ -97,6 +100,7 @@ SIGNATURES = [
     ("gol_partition_rows", ctypes.c_int, [_i64, _i64, _i64, _P(_i64), _P(_i64)]),
     ("gol_engine_create", ctypes.c_int, [_i64, _i64, _P(gol_config), _P(_vp)]),
     ("gol_rccl_unique_id", ctypes.c_int, [_vp, _i64]),
+    ("gol_ipc_unique_id", ctypes.c_int, [_vp, _i64]),
     ("gol_engine_create_rank", ctypes.c_int, [_i64, _i64, _i32, _i32, _vp, _P(gol_config), _P(_vp)]),
     ("gol_engine_destroy", None, [_vp]),
     ("gol_engine_topology", ctypes.c_int, [_vp, _P(_i32), _P(_i32), _P(_i32), _P(_i32)]),

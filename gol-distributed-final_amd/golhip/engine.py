@@ -6,7 +6,8 @@ count, alive list, the board bytes, a PGM snapshot) are served from the device.
 The board may be row-sharded over several GPUs (broker.go:135-206's partition
 applied to GPUs) with a k-row halo exchange per launch: `shards=` in one process
 (RCCL between distinct GPUs, device copies between shards sharing a GPU), or
-`Engine.rank(...)` with one process per GPU (RCCL).
+`Engine.rank(...)` with one process per GPU (RCCL; or HIP IPC between the processes of one node,
+which may share a GPU).
 """
 from __future__ import annotations
 
@@ -14,7 +15,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_STEP_PERSIST, GOL_WRITE_FN, LAYOUTS, STEP_MODES,
+from ._lib import (GOL_IPC_ID_BYTES, GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_WRITE_FN, LAYOUTS, STEP_MODES,
                    TRANSPORT_NAMES, TRANSPORTS, GolError, check, gol_config, lib)
 
 
@@ -28,34 +29,48 @@ def rccl_unique_id(library=None) -> bytes:
     return bytes(buf)
 
 
+def ipc_unique_id(library=None) -> bytes:
+    """A fresh id for Engine.rank(..., transport="ipc") (gol_ipc_unique_id: host only, no GPU);
+    share it with every rank."""
+    L = library or lib()
+    buf = (ctypes.c_uint8 * GOL_IPC_ID_BYTES)()
+    rc = L.gol_ipc_unique_id(buf, GOL_IPC_ID_BYTES)
+    if rc:
+        raise GolError(rc, L.gol_last_error().decode(errors="replace"))
+    return bytes(buf)
+
+
+def unique_id(transport: str = "rccl", library=None) -> bytes:
+    """The id Engine.rank needs for `transport` ("rccl" or "ipc")."""
+    return ipc_unique_id(library) if transport == "ipc" else rccl_unique_id(library)
+
+
 class Engine:
     def __init__(self, height: int, width: int, *, turns_per_launch: int = 0, cells_per_lane: int = 0,
                  strip_rows: int = 0, device: int = -1, layout: str = "auto", shards: int = 1,
-                 transport: str = "auto", same_device: bool = False, step: str = "auto", persist: bool = False,
-                 library=None, _rank=None):
-        # persist=True: the persistent multi-round launch of a one-shard band board (GOL_STEP_PERSIST,
-        # DESIGN.md §4.7) instead of one launch per k-turn step
+                 transport: str = "auto", same_device: bool = False, step: str = "auto", library=None, _rank=None):
         self.H, self.W = int(height), int(width)
         self._L = library or lib()
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, strip_rows=strip_rows,
                          cells_per_lane=cells_per_lane, layout=LAYOUTS[layout], shards=shards,
                          transport=TRANSPORTS[transport],
-                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | STEP_MODES[step] |
-                         (GOL_STEP_PERSIST if persist else 0))
+                         flags=(GOL_SHARDS_SAME_DEVICE if same_device else 0) | STEP_MODES[step])
         h = ctypes.c_void_p()
         if _rank is None:
             self._check(self._L.gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))
         else:
             nranks, rank, uid = _rank
-            idbuf = (ctypes.c_uint8 * GOL_RCCL_ID_BYTES).from_buffer_copy(uid) if uid is not None else None
+            idbuf = (ctypes.c_uint8 * len(uid)).from_buffer_copy(uid) if uid is not None else None
             self._check(self._L.gol_engine_create_rank(self.H, self.W, nranks, rank, idbuf, ctypes.byref(cfg),
                                                        ctypes.byref(h)))
         self._h = h
 
     @classmethod
     def rank(cls, height: int, width: int, nranks: int, rank: int, uid: bytes | None, **kw) -> "Engine":
-        """This process's shard `rank` of an `nranks`-rank board (one process per GPU, RCCL halo
-        exchange; collective: every rank constructs it with the same uid)."""
+        """This process's shard `rank` of an `nranks`-rank board (collective: every rank constructs
+        it with the same uid).  transport="rccl" (default with nranks > 1: one process per GPU, uid
+        from rccl_unique_id) or "ipc" (processes of one node that may share a GPU, uid from
+        ipc_unique_id)."""
         return cls(height, width, _rank=(nranks, rank, uid), **kw)
 
     def _check(self, rc: int) -> None:

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GOL_ABI_VERSION 3
+#define GOL_ABI_VERSION 4
 
 enum {
     GOL_OK = 0,
@@ -94,8 +94,14 @@ int gol_partition_rows(int64_t H, int64_t parts, int64_t i, int64_t *y0, int64_t
  *    `rank` of `nranks`; whole-board queries (alive count, hash, PGM write,
  *    counted steps) are collective: every rank calls them.
  * Transports of the halo rows: RCCL ncclSend/ncclRecv on a per-shard comm
- * stream (xGMI between GPUs), or LOOPBACK device copies between the shards of
- * one process (shards may share a GPU: multi-shard logic on a 1-GPU box). */
+ * stream (xGMI between GPUs), LOOPBACK device copies between the shards of
+ * one process (shards may share a GPU: multi-shard logic on a 1-GPU box), or
+ * IPC between the rank processes of one node: each rank copies its ghost rows
+ * out of its neighbours' HBM through HIP IPC mappings, ordered by sequence
+ * flags in device memory, and the collectives (counts, error words, barriers)
+ * run on the host through a shared-memory segment.  IPC ranks may share a GPU
+ * (RCCL refuses two ranks on one GPU), so the one-process-per-GPU engine runs
+ * with 2-16 processes on a 1-GPU box exactly as it runs on 8 GPUs. */
 typedef struct gol_engine gol_engine;
 
 /* Bit-board layout used while stepping.  STANDARD: word s of a row holds cells
@@ -110,15 +116,14 @@ typedef struct gol_engine gol_engine;
 #define GOL_TRANSPORT_AUTO 0     /* 1 shard: local torus wrap; shards on distinct GPUs: RCCL; else LOOPBACK */
 #define GOL_TRANSPORT_LOOPBACK 1 /* device copies between the shards of this process */
 #define GOL_TRANSPORT_RCCL 2     /* ncclSend/ncclRecv (with one shard: send to self) */
-#define GOL_TRANSPORT_LOCAL 3    /* (reported only) one shard, wrap rows copied on its own stream */
+#define GOL_TRANSPORT_LOCAL 3    /* (reported only) one shard, wrap rows read from the board itself */
+#define GOL_TRANSPORT_IPC 4      /* gol_engine_create_rank only: HIP IPC halo pulls + host collectives */
 /* gol_config.flags */
 #define GOL_SHARDS_SAME_DEVICE 1 /* every local shard on `device` (loopback testing on one GPU) */
 #define GOL_STEP_SERIAL 2        /* one launch per shard and step, after the halo exchange (gol_step_plan) */
 #define GOL_STEP_EDGE_FIRST 4    /* the edge rows first on the compute stream, then the interior (gol_step_plan) */
 #define GOL_STEP_OVERLAP 8       /* the edge rows on the edge stream beside the interior (gol_step_plan) */
-#define GOL_STEP_PERSIST 16      /* one shard in the band layout at k = 12: many steps per launch (the
-                                    persistent multi-round kernel; measured slower or
-                                    equal, so opt-in) */
+                                 /* (16: ABI 3's persistent multi-round launch, removed in ABI 4) */
 typedef struct gol_config {
     int32_t device;           /* HIP device ordinal (first shard); -1 = current device */
     int32_t turns_per_launch; /* k (temporal blocking); 0 = library default */
@@ -132,11 +137,20 @@ typedef struct gol_config {
 
 int gol_engine_create(int64_t H, int64_t W, const gol_config *cfg, gol_engine **out);
 /* One process per GPU: every rank calls this (collective) with the same H, W,
- * nranks and unique id (from gol_rccl_unique_id on one rank, shared by the
- * caller's own means, e.g. torch.distributed or the Go broker's RPC).  cfg->device
- * is this rank's GPU.  Needs W % 64 == 0 and H >= nranks. */
+ * nranks and unique id, made on one rank and shared by the caller's own means
+ * (e.g. torch.distributed or the Go broker's RPC): gol_rccl_unique_id for
+ * cfg->transport GOL_TRANSPORT_RCCL (the default with nranks > 1),
+ * gol_ipc_unique_id for GOL_TRANSPORT_IPC (at most GOL_IPC_MAX_RANKS ranks, one
+ * node; the id names the ranks' shared-memory segment, which exists only while
+ * they connect).  cfg->device is this rank's GPU (IPC ranks may name the same
+ * one).  Needs W % 64 == 0 and H >= nranks.  With several ranks every stepping
+ * call starts by agreeing on the halo state: a rank whose rows changed outside
+ * a step (load_words on it alone) makes every rank exchange its halo again. */
 #define GOL_RCCL_ID_BYTES 128
+#define GOL_IPC_ID_BYTES 128
+#define GOL_IPC_MAX_RANKS 16
 int gol_rccl_unique_id(uint8_t *id, int64_t len);
+int gol_ipc_unique_id(uint8_t *id, int64_t len);
 int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int32_t rank, const uint8_t *id,
                            const gol_config *cfg, gol_engine **out);
 void gol_engine_destroy(gol_engine *e);

@@ -58,7 +58,7 @@ def test_header_compiles(tmp_path, compiler, lang):
 
 
 def test_abi_version(G):
-    assert G.lib().gol_abi_version() == 3
+    assert G.lib().gol_abi_version() == 4
 
 
 @pytest.mark.parametrize("H,T", [(512, 4), (512, 16), (16, 3), (64, 7), (17, 5), (10, 16), (1, 1), (0, 3)])

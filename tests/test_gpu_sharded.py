@@ -147,15 +147,16 @@ def _bench_line(args):
     return json.loads(lines[0])
 
 
-def test_bench_self_launch_two_ranks():
-    """`python bench.py --gpus 2` with no launcher: the parent starts 2 ranks before touching the
-    GPU; with --share-gpu (RCCL refuses two ranks on one GPU) each rank steps its own replica of
-    the rows_per_gpu-row torus, so the line must report 2x the one-rank alive count and the
-    whole-job rate from the max-over-ranks time."""
+def test_bench_self_launch_two_replicas():
+    """`python bench.py --gpus 2 --workload bit64k` with no launcher: the parent starts 2 ranks
+    before touching the GPU; bit64k is a one-GPU workload, so each rank steps its own replica of
+    the 65536^2 torus: the line must report 2x the one-rank alive count and the whole-job rate
+    from the max-over-ranks time.  (The sharded workloads with --share-gpu run the rank engine
+    over IPC: tests/test_gpu_ranks.py.)"""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    common = ["--rows-per-gpu", "2048", "--width", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    common = ["--workload", "bit64k", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
     two = _bench_line(["--gpus", "2", "--share-gpu"] + common)
     one = _bench_line(common)
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
@@ -163,5 +164,5 @@ def test_bench_self_launch_two_ranks():
     assert two["config"]["turns_done"] == one["config"]["turns_done"]
     assert two["config"]["alive_final"] == 2 * one["config"]["alive_final"]
     k = one["config"]["turns_per_step"]
-    assert abs(two["value"] - 2 * 2048 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
+    assert abs(two["value"] - 2 * 65536 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
     assert one["roofline"]["launch_ms"] > 0 and one["config"]["timed_launches"] == 3
