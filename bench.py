@@ -236,6 +236,7 @@ def roofline(kind, launch_ms, cell_updates, pmc, pmc_note):
                   # the same kernel at the shader clock its profile measured (the chip lowers its
                   # clock under this load: power), and its work per instruction
                   "profile_clock_GHz": pmc.get("clock_GHz"),
+                  "profile_clock_source": pmc.get("clock_source"),
                   "frac_at_profile_clock": round(ach / (VALU_PEAK_GINST / 2.4 * pmc["clock_GHz"]), 4)
                   if pmc.get("clock_GHz") else None,
                   "cell_updates_per_valu_lane_op": round(cell_updates / (valu * 64), 3),

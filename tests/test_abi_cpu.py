@@ -61,6 +61,19 @@ def test_abi_version(G):
     assert G.lib().gol_abi_version() == 4
 
 
+def test_ipc_unique_id_host_only(G):
+    """gol_ipc_unique_id needs no GPU: 128 bytes, the IPC magic, 16 random bytes naming the ranks'
+    shared-memory segment; two ids differ; a short buffer is EINVAL."""
+    import ctypes
+    a, b = G.engine.ipc_unique_id(), G.engine.ipc_unique_id()
+    assert len(a) == len(b) == G._lib.GOL_IPC_ID_BYTES == 128
+    assert a[:8] == b"GOLIPC1\0" and b[:8] == a[:8]
+    assert a[8:24] != b[8:24] and a[24:] == bytes(104)
+    assert G.engine.unique_id("ipc")[:8] == a[:8]
+    buf = (ctypes.c_uint8 * 16)()
+    assert G.lib().gol_ipc_unique_id(buf, 16) == G._lib.GOL_EINVAL
+
+
 @pytest.mark.parametrize("H,T", [(512, 4), (512, 16), (16, 3), (64, 7), (17, 5), (10, 16), (1, 1), (0, 3)])
 def test_partition_matches_broker_formula(G, H, T):
     for i in range(T):

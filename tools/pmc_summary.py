@@ -5,7 +5,12 @@ and update profiles/pmc_traffic.json, read by bench.py for the roofline (HBM byt
 VALU instructions per launch of the step kernel).  Each entry records the sha256 prefix of the
 gol_kernels.hip it was measured on; bench.py ignores an entry whose hash differs.
 
-    python tools/pmc_summary.py <tag> <bench key, e.g. weak:131072x1048576:k12:band>
+    python tools/pmc_summary.py <tag> <bench key, e.g. weak:131072x1048576:k12:band> [--clock GHZ]
+
+The shader clock of a dispatch is GRBM_GUI_ACTIVE / 8 / its duration (rocprofv3 sums the 8 XCDs),
+which reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, 'DVFS give-back'): for
+those the clock is taken only from --clock (the in-kernel s_memtime / s_memrealtime median of
+tools/timeline.py clock), else left null.
 
 HBM bytes per launch = FETCH_SIZE*2 + WRITE_SIZE (KiB -> bytes), the gfx950 correction of
 MI355X_MICROARCH.md §HBM (FETCH_SIZE reports half of a wide streaming read)."""
@@ -19,6 +24,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag, key = sys.argv[1], sys.argv[2]  # e.g. r01 weak:131072x1048576:n1:k16:cpl0 (bench.py load_pmc key)
+CLOCK = float(sys.argv[sys.argv.index("--clock") + 1]) if "--clock" in sys.argv else None
+SHORT_NS = 300e3  # below this the GRBM quotient is not a clock
 src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
 dst = os.path.join(ROOT, "profiles", tag)
 os.makedirs(dst, exist_ok=True)
@@ -57,10 +64,15 @@ for k, c in means.items():
         if ns:
             e["hbm_GBs"] = b / ns
     if "GRBM_GUI_ACTIVE" in c and ns:
-        e["clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / ns
-        if "SQ_INSTS_VALU" in c:
-            cyc = c["GRBM_GUI_ACTIVE"] / 8
-            e["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (256 * 4 * 0.5 * cyc)
+        e["grbm_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / ns
+        if CLOCK:
+            e["clock_GHz"], e["clock_source"] = CLOCK, "in-kernel s_memtime / s_memrealtime (tools/timeline.py clock)"
+        elif ns >= SHORT_NS:
+            e["clock_GHz"], e["clock_source"] = e["grbm_clock_GHz"], "GRBM_GUI_ACTIVE / 8 / trace duration"
+        else:
+            e["clock_GHz"], e["clock_source"] = None, "dispatch < 0.3 ms: the GRBM quotient reads high; no in-kernel clock given"
+        if "SQ_INSTS_VALU" in c and e["clock_GHz"]:
+            e["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (256 * 4 * 0.5 * e["clock_GHz"] * ns)
     out[k] = e
 json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 if not out:
@@ -81,6 +93,8 @@ if "hbm_bytes_per_launch" in out[main]:
     if "valu_issue_frac" in out[main]:
         t[key]["valu_issue_frac_profile_clock"] = round(out[main]["valu_issue_frac"], 4)
     if "clock_GHz" in out[main]:
-        t[key]["clock_GHz"] = round(out[main]["clock_GHz"], 3)
+        ck = out[main]["clock_GHz"]
+        t[key]["clock_GHz"] = round(ck, 3) if ck else None
+        t[key]["clock_source"] = out[main]["clock_source"]
     json.dump(t, open(tp, "w"), indent=1)
 print(json.dumps(out[main], indent=1))

@@ -8,6 +8,11 @@ span the waves are resident, the dispatch ramp, and the tail.
 
     python tools/timeline.py build [-DFLAG=..]     # here (hipcc), -> tools/tl/libtimeline.so
     python tools/timeline.py run bit64k|byte16k|weak [--strip N]   # on the GPU box
+    python tools/timeline.py build -DGOL_EXP_CLOCK && python tools/timeline.py clock WORKLOAD
+        # the shader clock under load: every wave's s_memtime / s_memrealtime (100 MHz) deltas over
+        # its life in the last of >= 2 s of back-to-back launches on a random board (median over
+        # waves; MI355X_MICROARCH.md 'DVFS give-back' item 6), for dispatches too short for
+        # GRBM_GUI_ACTIVE / 8 / time
 """
 import json
 import os
@@ -22,8 +27,7 @@ LIB = os.environ.get("GOL_TL_LIB") or os.path.join(ROOT, "tools", "tl", "libtime
 
 ENTRY = "    const int lane = threadIdx.x & 63;\n"
 STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n    const uint64_t tl_c0 = __builtin_amdgcn_s_memtime(); (void)tl_c0;\n"
-EXIT_BAND = "    if (COUNT && wv == P - 1) slot_add(a.slots, alive);\n}"
-EXIT_BYTES = "    if (!ok) raise_error(a.err, GOLK_ERR_SPIN);\n    if (COUNT && wv == P - 1) slot_add(a.slots, alive);\n}"
+COUNT_LINE = "    if (COUNT && wv == P - 1) slot_add(a.slots, alive);\n"
 STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear workgroup id * P + wave
         const uint64_t tl_t1 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -34,13 +38,15 @@ STORE = """    {  // timeline: (t0, t1, hw_id, xcc_id) per wave, slot = linear w
 #ifdef GOL_EXP_PROF
             a.slots[4 * i] = tl_c0; a.slots[4 * i + 1] = __builtin_amdgcn_s_memtime();
             a.slots[4 * i + 2] = prof_a; a.slots[4 * i + 3] = prof_b | ((uint64_t)wv << 56); (void)hw; (void)xcc;
+#elif defined(GOL_EXP_CLOCK)
+            a.slots[4 * i + 2] = tl_c0; a.slots[4 * i + 3] = __builtin_amdgcn_s_memtime(); (void)hw; (void)xcc;
 #else
             a.slots[4 * i + 2] = hw; a.slots[4 * i + 3] = xcc | ((uint64_t)wv << 56) | ((uint64_t)(threadIdx.x >> 6) << 48);
 #endif
         }
         (void)alive;
     }
-}"""
+"""
 
 
 PROF_SPINS = (  # -DGOL_EXP_PROF: cycles each wave spends in its flag waits (ready -> a, free -> b)
@@ -64,13 +70,12 @@ def build(flags=""):
             i = src.index(kern)
             j = src.index("    uint32_t alive = 0;\n", i)
             src = src[:j] + "    uint64_t prof_a = 0, prof_b = 0;\n" + src[j:]
-    for kern, exit_ in (("band_pipe_kernel(BitsArgs a)", EXIT_BAND), ("bytes_pipe_kernel(BytesKArgs a)", EXIT_BYTES)):
+    for kern in ("band_pipe_kernel(BitsArgs a)", "bytes_pipe_kernel(BytesKArgs a)"):
         i = src.index(kern)
         j = src.index(ENTRY, i)
         src = src[:j] + STAMP_T0 + src[j + len(ENTRY):]
-        k = src.index(exit_, j)
-        count_line = exit_[exit_.rindex("    if ("):]  # the kernel's final slot_add (and closing brace)
-        src = src[:k] + exit_.replace(count_line, STORE) + src[k + len(exit_):]
+        k = src.index(COUNT_LINE, j)  # the kernel's final fused-count slot_add: the stamps replace it
+        src = src[:k] + STORE + src[k + len(COUNT_LINE):]
     open(os.path.join(OUT, "gol_kernels.hip"), "w").write(src)
     for f in os.listdir(CSRC):
         if f.endswith((".cpp", ".h")) or f == "Makefile":
@@ -175,7 +180,70 @@ def run(workload, strip):
     np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{workload}_{strip}.npy"), v)
 
 
+def clock(workload, seconds=2.0):
+    """Median in-kernel shader clock of the step kernel of `workload` on a random board."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gol-distributed-final_amd")]
+    import time
+
+    import numpy as np
+    import torch
+
+    import golhip._lib as L
+    lib = L.load(LIB)
+    st = torch.cuda.current_stream().cuda_stream
+    if workload == "byte16k":
+        H = W = 16384
+        k, P = 32, 8
+        bits = torch.empty((H, W // 32), dtype=torch.int32, device="cuda")
+        assert lib.gol_dev_random_fill(bits.data_ptr(), H, 0, W, W // 32, 1, st) == 0
+        a = torch.empty((H, W), dtype=torch.uint8, device="cuda")
+        assert lib.gol_dev_unpack(bits.data_ptr(), H, W, W // 32, a.data_ptr(), W, st) == 0
+        b = torch.empty_like(a)
+        buf = torch.zeros(4 * P * ((W // 32 + 61) // 62) * H, dtype=torch.int64, device="cuda")
+        bufs = [(a, b), (b, a)]
+        launch = lambda s, d: lib.gol_dev_bytes_step_k(s[H - k:].data_ptr(), s.data_ptr(), s.data_ptr(), d.data_ptr(),  # noqa: E731
+                                                       H, W, W, 0, H, k, 0, buf.data_ptr(), st)
+    else:
+        H, W = {"bit64k": (65536, 65536), "weak": (1 << 17, 1 << 20), "strong262k": (262144, 262144)}[workload]
+        k, P = 12, 16
+        Wd = W // 32
+        a = torch.empty((H, Wd), dtype=torch.int32, device="cuda")
+        b = torch.empty_like(a)
+        assert lib.gol_dev_random_fill(a.data_ptr(), H, 0, W, Wd, 1, st) == 0
+        buf = torch.zeros(4 * P * ((Wd + 231) // 232) * H, dtype=torch.int64, device="cuda")
+        bufs = [(a, b), (b, a)]
+        launch = lambda s, d: lib.gol_dev_band_step(s[H - k:].data_ptr(), s.data_ptr(), s.data_ptr(), d.data_ptr(),  # noqa: E731
+                                                    H, Wd, Wd, 0, H, k, 128, 0, buf.data_ptr(), st)
+    torch.cuda.synchronize()
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:  # back-to-back launches (the board evolves: random data)
+        for _ in range(8):
+            s, d = bufs[n & 1]
+            assert launch(s, d) == 0
+            n += 1
+        torch.cuda.synchronize()
+    buf.zero_()
+    s, d = bufs[n & 1]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    assert launch(s, d) == 0
+    e1.record()
+    torch.cuda.synchronize()
+    v = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+    v = v[(v[:, 1] > v[:, 0]) & (v[:, 3] > v[:, 2])]
+    ghz = (v[:, 3] - v[:, 2]) / ((v[:, 1] - v[:, 0]) / 100.0) / 1e3  # cycles per us / 1000
+    out = {"workload": workload, "launches_before": n, "event_ms": round(e0.elapsed_time(e1), 4), "waves": int(len(v)),
+           "clock_GHz_median": round(float(np.median(ghz)), 3),
+           "clock_GHz_pct": [round(float(np.percentile(ghz, q)), 3) for q in (5, 25, 50, 75, 95)],
+           "method": "per wave: delta s_memtime / delta s_memrealtime x 100 MHz over its life, in the last of "
+                     f"{n + 1} back-to-back launches ({seconds} s) on a random board"}
+    print(json.dumps(out), flush=True)
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "clock":
+        clock(sys.argv[2])
+        sys.exit(0)
     if sys.argv[1] == "build":
         build(" ".join(sys.argv[2:]))  # extra compiler flags, e.g. -DGOL_PIPE_Q=1
     else:
