@@ -1402,8 +1402,8 @@ static int pgm_stream(gol_engine *e, gol_write_fn sink, void *user, int64_t *hle
     char header[96];
     const int hlen = snprintf(header, sizeof header, "P5\n%lld %lld\n255\n", (long long)e->W, (long long)e->H);  // io.go:52-59
     *hlen_out = hlen;
-    const bool several = e->rank_mode && e->nranks > 1;
-    if (!several || e->rank == 0) {
+    const bool coll = several(e);
+    if (!coll || e->rank == 0) {
         if (sink(user, 0, (const uint8_t *)header, hlen) != 0) return gol_set_error(GOL_EIO, "the PGM sink failed (header)");
     }
     for (auto &s : e->sh) {
@@ -1483,9 +1483,9 @@ extern "C" int gol_engine_write_pgm_to(gol_engine *e, gol_write_fn sink, void *u
 extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
 {
     if (!e || !path) return gol_set_error(GOL_EINVAL, "bad arguments");
-    const bool several = e->rank_mode && e->nranks > 1;
+    const bool coll = several(e);
     int rc = GOL_OK;
-    if (!several || e->rank == 0) {
+    if (!coll || e->rank == 0) {
         char header[96];
         const int hlen = snprintf(header, sizeof header, "P5\n%lld %lld\n255\n", (long long)e->W, (long long)e->H);
         const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
@@ -1495,7 +1495,7 @@ extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
             if (close(fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
         }
     }
-    if (several) {
+    if (coll) {
         const int rb = rank_barrier(e);  // the file exists and is sized before any rank writes
         if (rc == GOL_OK) rc = rb;
     }
@@ -1507,7 +1507,7 @@ extern "C" int gol_engine_write_pgm(gol_engine *e, const char *path)
         if (rc == GOL_EIO) gol_set_error(GOL_EIO, "short write to %s", path);
     }
     if (fs.fd >= 0 && close(fs.fd) != 0 && rc == GOL_OK) rc = gol_set_error(GOL_EIO, "close %s", path);
-    if (several) {
+    if (coll) {
         const int rb = rank_barrier(e);  // every rank's rows are written when any rank returns
         if (rc == GOL_OK) rc = rb;
     }
