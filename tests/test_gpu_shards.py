@@ -325,6 +325,25 @@ def test_timing_counts_the_step_launches(G):
         assert t["mean_cell_updates"] == 300 * 2048 * 12
 
 
+def test_timing_then_flips_outside_a_timed_call(G):
+    """with timing on, a step_flips call (not a timed stepping call) must not write the
+    per-call timing arrays (it used to index them out of bounds when no step had run) and must not
+    count as a timed step."""
+    H, W = 200, 2048
+    words = O.random_words(2, 0, H, W // 64)
+    with G.Engine(H, W, device=0) as e:
+        e.load_random(2)
+        e.set_timing(True)
+        flips = e.step_flips()
+        assert e.timing()["launches"] == 0
+        e.step(12)
+        assert e.timing()["launches"] == 1
+        ref1 = O.bits_run(words, 1)
+        want = O.flipped_cells(O.unpack(words), O.unpack(ref1))
+        assert [tuple(x) for x in flips.tolist()] == [tuple(x) for x in want]
+        assert e.hash() == O.hash_words(O.bits_run(ref1, 12))
+
+
 def test_device_fault_is_reported(G):
     """A pipeline wave that gives up waiting (the test build libgolhip_spintest.so times out every
     flag wait at once) must surface as GOL_EHIP, not as a board with unwritten strips (child
