@@ -498,7 +498,10 @@ static int plan_of(gol_engine *e, int i, gol_halo_op (&ops)[4])
 // matching of the same plan, including nranks = 2 (one peer on both sides) and the one-shard
 // torus wrap (a shard sending to itself).
 // One shard that is the whole torus (LOCAL transport): the step launches read the wrap rows from
-// the board itself (step_launch), so there is nothing to exchange.
+// the board itself (step_launch), so there is nothing to exchange.  (Copying them into the ghost
+// rows beside the interior instead, for the contiguous-row kernel that ran 1.3-2 % faster in
+// tools/step_cost.py, measured -0.5 % on the weak board through bench.py, same box:
+// profiles/r04/r04d_ab_steps.jsonl.)
 static bool local_wrap(const gol_engine *e)
 {
     return e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;

@@ -2259,12 +2259,12 @@ hipError_t golk_reset_claims_device(int device)
 }
 
 static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const double *weight, int64_t min_rows,
-                       int64_t max_strip, StripMap &sm, uint32_t *claims = nullptr, int chunk = 0)
+                       int64_t max_strip, StripMap &sm, uint32_t *claims = nullptr, int chunk = 0, int max_rounds = 2)
 {
     if (cus <= 0 || cus % 8 || per_cu < 1 || per_cu > 4 || ngroups > cus || rows <= 0) return false;
-    // only boards that fill the device at most twice with strips of max_strip rows: on bigger
-    // boards workgroups refill the CUs as they finish, and only the last round has the tail
-    if (ngroups * ((rows + max_strip - 1) / max_strip) > 2 * (int64_t)cus * per_cu) return false;
+    // only boards that fill the device at most max_rounds times with strips of max_strip rows: on
+    // bigger boards workgroups refill the CUs as they finish, and only the last round has the tail
+    if (ngroups * ((rows + max_strip - 1) / max_strip) > max_rounds * (int64_t)cus * per_cu) return false;
     const int64_t t = cus / ngroups;  // strips per column group, one CU each
     if (t * ngroups * 100 < (int64_t)cus * 94) return false;
     const int64_t period = (rows + t - 1) / t;
@@ -2353,6 +2353,14 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 #define GOL_BYTES_PIPE_P 8
 #endif
 #define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
+// Band launches of up to this many rounds of 1024-row strips run as one round of rank-weighted,
+// paired ranges instead (a 65536 x 262144 shard, config 4's share at N = 4: 2.95 rounds of 781-row
+// strips measured 132-133 TCUPS against 139-142 for the one-round 32768-row and the 9-round
+// 131072-row shards, profiles/r04/r04c_step_plans.jsonl)
+#ifndef GOL_BAND_RANK_ROUNDS
+#define GOL_BAND_RANK_ROUNDS 4
+#endif
+static constexpr int BAND_RANK_ROUNDS = GOL_BAND_RANK_ROUNDS;
 static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
 
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
@@ -2368,9 +2376,11 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
     const int64_t slots = resident_workgroups(kf, 64 * P);
     if (auto_strip && cus > 0 &&
         rank_split(a.rows, a.ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, a.sm,
-                   GOL_BAND_PAIRED ? claim_counters(s, cus) : nullptr, 3)) {
+                   GOL_BAND_PAIRED ? claim_counters(s, cus) : nullptr, 3, BAND_RANK_ROUNDS) &&
+        (int64_t)a.sm.period * a.pitch * 4 < (int64_t(1) << 31)) {  // (a range's stores: one 32-bit buffer)
         nwg = (int64_t)cus * a.sm.per_cu;
     } else {
+        a.sm = StripMap{};  // (rank_split may have filled it before the range check failed)
         if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
         nwg = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
         if (auto_strip && GOL_BAND_TAIL > 0 && slots > 0 && nwg > 4 * slots) {

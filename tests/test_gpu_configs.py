@@ -103,6 +103,23 @@ def test_config4_262144_full_board(G):
         _free_engine(e)
 
 
+@pytest.mark.parametrize("H,W", [(65536, 262144), (32768, 262144), (131072, 262144)])
+def test_config4_rank_shares_tiled(G, H, W):
+    """Config 4's per-rank shares at N = 4, 8 and 2 (65536, 32768, 131072 rows x 262144): the
+    first two run as one round of rank-weighted, paired ranges (the 65536-row share since round 4,
+    GOL_BAND_RANK_ROUNDS), the third as 9 rounds of strips; through the serial and the overlapped
+    step plan of a one-rank RCCL engine (the plan of the N-GPU run: ghost rows from the exchange,
+    contiguous rows), counted every 12 turns, every tile against the oracle."""
+    tile, ref, counts = _tile(43, 256, 1024, 36, 12)
+    reps = (H // 256) * (W // 1024)
+    for step in ("serial", "overlap"):
+        with G.Engine.rank(H, W, 1, 0, G.engine.rccl_unique_id(), device=0, transport="rccl", step=step) as e:
+            _load_tiled(e, H, W, tile)
+            assert e.step_counted(36, 12).tolist() == [reps * c for c in counts]
+            _check_tiled(e, H, W, ref, chunk_rows=16384)
+            _free_engine(e)
+
+
 def test_config5_bench_workload_exact(G):
     """The bench's exact workload (bench.py, seed 1, 2^17 x 2^20, 5 + 20 k = 12 launches with the
     count fused into every launch) as a CROSS-KERNEL check: the 25 counts and the final hash of the
