@@ -109,6 +109,7 @@ struct gol_engine {
     int step_flags = 0;        // GOL_STEP_SERIAL
     bool halo_ok = false;      // the ghost rows of bits[cur] hold the current halo (kx rows)
     bool halo_issued = false;  // an exchange was enqueued since the last synchronisation point
+    bool halo_on_compute = false;  // the last exchange ran on the compute streams (RCCL after a SERIAL step)
     bool timing = false;
     std::vector<gol_timed> timed;
     std::vector<size_t> tcall_ev;      // the current stepping call's start events (one per shard)

@@ -43,9 +43,10 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
                           int64_t Wd, int64_t pitch, int64_t row0, int64_t rows, int k, int dw, int strip,
                           uint64_t *slots, uint32_t *err, hipStream_t s);
 int golk_band_useful_words(int k, int dw);
-// Rounds of resident workgroups a step launch over `rows` rows makes (the band pipeline; other
-// kernels: 1e9, i.e. many); for the engine's choice of step plan.
-double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int strip);
+// Rounds of resident workgroups a step launch over `rows` rows makes (the band pipeline: 1 for
+// its one-round rank-weighted launch; other kernels: 1e9, i.e. many); for the engine's choice of
+// step plan.
+double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int64_t pitch, int k, int dw, int strip);
 // Standard <-> band rows (Wd % 32 == 0), out of place.
 hipError_t golk_band_convert(bool to_band, const uint32_t *src, uint32_t *dst, int64_t rows, int64_t Wd,
                              int64_t spitch, int64_t dpitch, hipStream_t s);

@@ -2259,7 +2259,8 @@ hipError_t golk_reset_claims_device(int device)
 }
 
 static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const double *weight, int64_t min_rows,
-                       int64_t max_strip, StripMap &sm, uint32_t *claims = nullptr, int chunk = 0, int max_rounds = 2)
+                       int64_t max_strip, StripMap &sm, bool paired, uint32_t *claims = nullptr, int chunk = 0,
+                       int max_rounds = 2)
 {
     if (cus <= 0 || cus % 8 || per_cu < 1 || per_cu > 4 || ngroups > cus || rows <= 0) return false;
     // only boards that fill the device at most max_rounds times with strips of max_strip rows: on
@@ -2275,7 +2276,7 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
     m.cus = cus;
     m.per_cu = per_cu;
     m.period = (int32_t)period;
-    if (claims && per_cu >= 2) {
+    if (paired && per_cu >= 2) {
         // pairs walking one range from both ends: per_cu 2: (0, 1); 3: (0, 2) + rank 1 alone;
         // 4: (0, 3) + (1, 2).  A pair's range gets the sum of its ranks' weights.
         static const int pa[4][2] = {{0, 0}, {0, 0}, {0, 1}, {0, 2}};
@@ -2353,15 +2354,38 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 #define GOL_BYTES_PIPE_P 8
 #endif
 #define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
-// Band launches of up to this many rounds of 1024-row strips run as one round of rank-weighted,
-// paired ranges instead (a 65536 x 262144 shard, config 4's share at N = 4: 2.95 rounds of 781-row
-// strips measured 132-133 TCUPS against 139-142 for the one-round 32768-row and the 9-round
-// 131072-row shards, profiles/r04/r04c_step_plans.jsonl)
+// Rows per strip of the band pipeline's launches of many rounds (same box, weak board, 3 reps:
+// 1024 148.4 TCUPS, 2048 148.3, 4096 147.0; profiles/r04/r04d_ab_rounds.jsonl)
+#ifndef GOL_BAND_STRIP
+#define GOL_BAND_STRIP 1024
+#endif
+// Band launches of up to this many rounds of strips run as one round of rank-weighted, paired
+// ranges instead, when their column groups spread over the CUs (rank_split).  Same box, 3 reps
+// each: config 4's N = 4 share 65536 x 262144 (2.95 rounds of 781-row strips) 134.2 -> 148.3
+// TCUPS at 4 rounds; at 16 rounds the N = 2 share 131072 x 262144 (4.5 rounds) 142.0 -> 150.2
+// and the whole 262144^2 board (9 rounds) 145.3 -> 149.4 (profiles/r04/r04d_ab_*.jsonl).  The
+// weak board's 133 column groups spread over 256 CUs only one per CU (52 %): strips.
 #ifndef GOL_BAND_RANK_ROUNDS
-#define GOL_BAND_RANK_ROUNDS 4
+#define GOL_BAND_RANK_ROUNDS 16
 #endif
 static constexpr int BAND_RANK_ROUNDS = GOL_BAND_RANK_ROUNDS;
 static constexpr int BYTES_PIPE_P = GOL_BYTES_PIPE_P;
+
+// The band pipeline's one-round launch (rank_split) of `rows` rows, when it applies; claims:
+// the paired ranks' counters (null: only ask whether it applies).
+static bool band_rank_map(int64_t rows, int64_t ngroups, int64_t pitch, int cus, int64_t slots, uint32_t *claims,
+                          StripMap &sm)
+{
+    constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
+    if (cus <= 0 || slots <= 0) return false;
+    StripMap m{};
+    if (!rank_split(rows, ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, m, GOL_BAND_PAIRED,
+                    claims, 3, BAND_RANK_ROUNDS))
+        return false;
+    if ((int64_t)m.period * pitch * 4 >= (int64_t(1) << 31)) return false;  // a range's stores: one 32-bit buffer
+    sm = m;
+    return true;
+}
 
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
@@ -2374,13 +2398,10 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
     int64_t nwg = 0;
     const int cus = device_cus();
     const int64_t slots = resident_workgroups(kf, 64 * P);
-    if (auto_strip && cus > 0 &&
-        rank_split(a.rows, a.ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, a.sm,
-                   GOL_BAND_PAIRED ? claim_counters(s, cus) : nullptr, 3, BAND_RANK_ROUNDS) &&
-        (int64_t)a.sm.period * a.pitch * 4 < (int64_t(1) << 31)) {  // (a range's stores: one 32-bit buffer)
+    uint32_t *claims = auto_strip && GOL_BAND_PAIRED && cus > 0 ? claim_counters(s, cus) : nullptr;
+    if (auto_strip && (claims || !GOL_BAND_PAIRED) && band_rank_map(a.rows, a.ngroups, a.pitch, cus, slots, claims, a.sm)) {
         nwg = (int64_t)cus * a.sm.per_cu;
     } else {
-        a.sm = StripMap{};  // (rank_split may have filled it before the range check failed)
         if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
         nwg = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
         if (auto_strip && GOL_BAND_TAIL > 0 && slots > 0 && nwg > 4 * slots) {
@@ -2397,7 +2418,10 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
         }
     }
     const dim3 g((unsigned)nwg), blk(64 * P);
-    if (a.sm.ranked) {  // one-round launch: row-grain hand-off flags
+#ifndef GOL_BAND_RANK_ROWF
+#define GOL_BAND_RANK_ROWF 1
+#endif
+    if (a.sm.ranked && GOL_BAND_RANK_ROWF) {  // one-round launch: row-grain hand-off flags
         if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, true>), g, blk, 0, s, a);
         else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, true>), g, blk, 0, s, a);
         else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, true>), g, blk, 0, s, a);
@@ -2447,7 +2471,7 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
             a.strip = (int)std::min<int64_t>(rows, std::max<int64_t>(2, work / 512));
         else
             a.strip = strip > 0 ? std::min(strip, GOL_MAX_STRIP)
-                                : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(1024, rows * a.ngroups / 2048)));
+                                : (int)std::min<int64_t>(rows, std::max<int64_t>(8 * k, std::min<int64_t>(GOL_BAND_STRIP, rows * a.ngroups / 2048)));
         // the pipe kernel's stores address a strip as one buffer (32-bit range)
         a.strip = (int)std::max<int64_t>(1, std::min<int64_t>(a.strip, (int64_t(1) << 30) / (pitch * 4)));
         return launch_band_pipe(contig, a, s, strip <= 0 && !small);
@@ -2461,13 +2485,15 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
 
 int golk_band_useful_words(int k, int dw) { return band_useful_words(k, dw); }
 
-double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int k, int dw, int strip)
+double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int64_t pitch, int k, int dw, int strip)
 {
     if (!band || dw != 4 || k != 12 || rows <= 0) return 1e9;
     const int64_t ngroups = (Wd + band_useful_words(k, dw) - 1) / band_useful_words(k, dw);
     const int64_t slots = resident_workgroups((const void *)band_pipe_kernel<GOL_BAND_KW, GOL_BAND_P, true, true>, 64 * GOL_BAND_P);
     if (slots <= 0) return 1e9;
-    const int64_t st = strip > 0 ? strip : 1024;  // launch_band_pipe's strips: up to 1024 rows
+    StripMap sm{};
+    if (strip <= 0 && band_rank_map(rows, ngroups, pitch, device_cus(), slots, nullptr, sm)) return 1.0;
+    const int64_t st = strip > 0 ? strip : GOL_BAND_STRIP;  // launch_band_pipe's strips
     return (double)(ngroups * ((rows + st - 1) / st)) / (double)slots;
 }
 
@@ -2537,7 +2563,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         const int64_t max_rows = std::max<int64_t>(1, ((int64_t(1) << 31) - 1) / pitch - 1);
         if (strip <= 0 && cus > 0 &&
             rank_split(rows, a.ngroups, cus, (int)std::min<int64_t>(GOL_BYTES_PER_CU, slots / cus), BYTES_PIPE_RANK_W,
-                       2 * k, 1024, a.sm, claims, 4) && a.sm.period <= max_rows) {
+                       2 * k, 1024, a.sm, claims != nullptr, claims, 4) && a.sm.period <= max_rows) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
             a.sm = StripMap{};

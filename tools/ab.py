@@ -43,12 +43,9 @@ def main():
                 print(json.dumps({"lib": lib, "rep": rep, "error": p.stderr[-800:]}), flush=True)
                 sys.exit(3)
             line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-            rec = {"lib": lib, "rep": rep, "value": line["value"], "ms_per_step": line["ms_per_step"],
+            rec = {"bench": a.bench, "lib": lib, "rep": rep, "value": line["value"], "ms_per_step": line["ms_per_step"],
                    "launch_ms": (line["roofline"] or {}).get("launch_ms"),
                    "alive_final": line["config"].get("alive_final")}
-            stats = [ln for ln in p.stderr.splitlines() if ln.startswith("persist-stats")]  # measurement builds
-            if stats:
-                rec["stats"] = stats[-1]
             print(json.dumps(rec), flush=True)
 
 

@@ -10,5 +10,5 @@ rm -rf "$D" && mkdir -p "$D"
 cp "$R"/gol-distributed-final_amd/csrc/{Makefile,*.cpp,*.h,*.hip} "$D/"
 make -s -j8 -C "$D" ARCH=gfx950 BUILD=./obj OUT=../lib$N.so INC=$R/include \
     CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -I$R/include -I. $F"
-rm -rf "$D/obj"
+rm -rf "$D"  # (the copied sources are not needed once built)
 echo "$R/tools/variants/lib$N.so"

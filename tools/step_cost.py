@@ -16,6 +16,7 @@ events: first launch of a shard-step to its last).  Variants:
   loopback1     one shard through the LOOPBACK transport (device copies of the plan)
   loopback2     two shards on the same GPU (each half the rows, concurrent)
   rccl1         one shard, RCCL send-to-self (the multi-GPU code path, one rank)
+  rccl1-overlap, rccl1-serial   the same with the step plan forced
 """
 import argparse
 import json
@@ -36,6 +37,8 @@ VARIANTS = {
     "loopback1": dict(transport="loopback"),
     "loopback2": dict(shards=2, same_device=True, transport="loopback"),
     "rccl1": dict(transport="rccl"),
+    "rccl1-overlap": dict(transport="rccl", step="overlap"),
+    "rccl1-serial": dict(transport="rccl", step="serial"),
 }
 
 
@@ -49,9 +52,13 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--nocount", action="store_true", help="plain steps (no fused alive count)")
     ap.add_argument("--zero", action="store_true", help="an all-dead board (same instructions, no bit toggling)")
+    ap.add_argument("--lib", default="", help="a measurement build of the library (tools/build_variant.sh)")
     a = ap.parse_args()
     import torch
     import golhip
+    if a.lib:
+        import golhip._lib as L
+        L._lib = L.load(os.path.join(ROOT, a.lib), strict=False)
     torch.cuda.set_device(0)
     H, W = BOARDS[a.board]
     ref = None
@@ -92,6 +99,7 @@ def main():
             if ref is None:
                 ref = (h, counts[-1:].tolist())
             line = {"board": a.board + ("-zero" if a.zero else ""), "variant": name + ("-nocount" if a.nocount else ""), "rep": rep, "k": k,
+                    "lib": a.lib or "lib",
                     "warm_steps": nw, "steps": steps,
                     "wall_ms_per_step": round(dt / steps * 1e3, 4), "step_ms": round(t["mean_ms"], 4),
                     "shard_steps": t["launches"], "TCUPS": round(H * W * k * steps / dt / 1e12, 2),

@@ -7,7 +7,9 @@ one launch of a workload and summarises when workgroups start and end: how much 
 span the waves are resident, the dispatch ramp, and the tail.
 
     python tools/timeline.py build [-DFLAG=..]     # here (hipcc), -> tools/tl/libtimeline.so
-    python tools/timeline.py run bit64k|byte16k|weak [--strip N]   # on the GPU box
+    python tools/timeline.py run bit64k|byte16k|weak|strong2|strong8|strong262k [--strip N] [--wrap] [--pre N]
+        # on the GPU box; --wrap: wrap rows read from the board (LOCAL launch), else ghost rows;
+        # --pre N: a fill kernel over N x 4096 floats right before the launch
     python tools/timeline.py build -DGOL_EXP_CLOCK && python tools/timeline.py clock WORKLOAD
         # the shader clock under load: every wave's s_memtime / s_memrealtime (100 MHz) deltas over
         # its life in the last of >= 2 s of back-to-back launches on a random board (median over
@@ -86,7 +88,7 @@ def build(flags=""):
     print(LIB)
 
 
-def run(workload, strip):
+def run(workload, strip, wrap=False, pre=0):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "gol-distributed-final_amd")]
     import ctypes
 
@@ -106,7 +108,8 @@ def run(workload, strip):
         launch = lambda: lib.gol_dev_bytes_step_k(a[H - k:].data_ptr(), a.data_ptr(), a.data_ptr(), b.data_ptr(), H, W,  # noqa: E731
                                                   W, 0, H, k, strip, buf.data_ptr(), st)
     else:
-        H, W = {"bit64k": (65536, 65536), "weak": (1 << 17, 1 << 20)}[workload]
+        H, W = {"bit64k": (65536, 65536), "weak": (1 << 17, 1 << 20), "strong2": (131072, 262144),
+                "strong8": (32768, 262144), "strong262k": (262144, 262144)}[workload]
         k, P = 12, 16  # buffer sized for up to 16 waves per work item
         Wd = W // 32
         g = 16
@@ -114,14 +117,21 @@ def run(workload, strip):
         b = torch.zeros_like(a)
         mid = a[g:g + H]
         ngroups = (Wd + 231) // 232
-        buf = torch.zeros(4 * P * ngroups * H, dtype=torch.int64, device="cuda")
-        launch = lambda: lib.gol_dev_band_step(a[g - k:].data_ptr(), mid.data_ptr(), a[g + H:].data_ptr(),  # noqa: E731
+        buf = torch.zeros(4 * P * ngroups * min(H, 8192), dtype=torch.int64, device="cuda")
+        # --wrap: the torus wrap rows read from the board itself (the LOCAL engine's launch);
+        # else from ghost rows right above and below (contiguous: the N-GPU launch)
+        top = mid[H - k:] if wrap else a[g - k:]
+        bot = mid if wrap else a[g + H:]
+        launch = lambda: lib.gol_dev_band_step(top.data_ptr(), mid.data_ptr(), bot.data_ptr(),  # noqa: E731
                                                b[g:].data_ptr(), H, Wd, Wd, 0, H, k, 128, strip, buf.data_ptr(), st)
+    pre_t = torch.empty(max(1, pre) * 4096, dtype=torch.float32, device="cuda")
     for _ in range(3):
         assert launch() == 0
     torch.cuda.synchronize()
     buf.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if pre:  # a kernel of some other grid right before the launch, on the same stream
+        pre_t.fill_(1.0)
     e0.record()
     assert launch() == 0
     e1.record()
@@ -143,7 +153,7 @@ def run(workload, strip):
         m = key == kk
         per_cu[int(kk)] = (int(m.sum()), float(e[m].max()))
     life = e - s
-    out = {"workload": workload, "strip": strip, "event_ms": round(ms, 4), "waves": int(len(v)), "span_us": round(float(span), 1),
+    out = {"workload": workload, "strip": strip, "wrap": wrap, "pre": pre, "event_ms": round(ms, 4), "waves": int(len(v)), "span_us": round(float(span), 1),
            "resident_frac": round(float(life.sum() / (span * 16 * 256)), 3),
            "start_us_pct": [round(float(np.percentile(s, q)), 1) for q in (0, 10, 50, 90, 99, 100)],
            "end_us_pct": [round(float(np.percentile(e, q)), 1) for q in (0, 1, 10, 50, 90, 100)],
@@ -177,7 +187,7 @@ def run(workload, strip):
                        for r in np.unique(role)}
         out["start_us_pct"] = out["end_us_pct"] = out["life_us_pct"] = None
     print(json.dumps(out))
-    np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{workload}_{strip}.npy"), v)
+    np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{workload}_{strip}_{int(wrap)}_{pre}.npy"), v)
 
 
 def clock(workload, seconds=2.0):
@@ -248,4 +258,5 @@ if __name__ == "__main__":
         build(" ".join(sys.argv[2:]))  # extra compiler flags, e.g. -DGOL_PIPE_Q=1
     else:
         strip = int(sys.argv[sys.argv.index("--strip") + 1]) if "--strip" in sys.argv else 0
-        run(sys.argv[2], strip)
+        pre = int(sys.argv[sys.argv.index("--pre") + 1]) if "--pre" in sys.argv else 0
+        run(sys.argv[2], strip, "--wrap" in sys.argv, pre)
