@@ -65,6 +65,11 @@ def parse(argv=None):
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="before the warmup steps, untimed steps of the same workload until the GPU has run "
+                         "this many seconds: the shader clock settles during the first ~0.1-0.2 s of load "
+                         "(DESIGN.md §6), and a short --warmup (the driver's 5 weak steps = 58 ms) left the "
+                         "first timed steps on a lower clock; reported as config.settle_steps (0 = off)")
     ap.add_argument("--snapshot", default="",
                     help="after the timed steps write the board as a P5 file here (every rank its own "
                          "rows, gol_engine_write_pgm: config 5's snapshot); reported, not part of value")
@@ -310,6 +315,7 @@ def run_bits(args, ranks):
     info = e.info()
     k = info["turns_per_launch"]
     e.load_random(1)
+    settle = settle_steps(args, ranks, lambda n: e.step_counted(n * k, k), torch_sync=False)
     if args.warmup:
         e.step_counted(args.warmup * k, k)
     ranks.barrier()
@@ -351,13 +357,34 @@ def run_bits(args, ranks):
                                    (f"replicas{world}" if world > 1 else "1gpu")),
            "transport": topo["transport"], "turns_per_step": k, "layout": layout,
            "cells_per_lane": info["cells_per_lane"], "strip_rows": args.strip or "auto",
-           "alive_count_every_step": True, "alive_final": alive, "turns_done": (args.warmup + args.steps) * k,
-           "timed_launches": t["launches"]}
+           "alive_count_every_step": True, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
+           "settle_steps": settle, "timed_launches": t["launches"]}
     if snap:
         cfg["snapshot"] = snap
     e.close()
     dtype = "u32 (bit-packed, 32 cells/word" + (", column-band layout)" if layout == "band" else ")")
     return value, dt, cfg, roof, dtype
+
+
+def settle_steps(args, ranks, run_n, torch_sync):
+    """Untimed steps before the warmup until the GPU has been busy for args.settle_s seconds (the
+    shader clock's settling time).  The count comes from one timed step, maxed over
+    the ranks, so every rank runs the same steps (the sharded steps are collective)."""
+    if args.settle_s <= 0:
+        return 0
+    import torch
+
+    def timed(n):
+        t0 = time.perf_counter()
+        run_n(n)
+        if torch_sync:
+            torch.cuda.synchronize()
+        return time.perf_counter() - t0
+    dt = ranks.max(timed(1))
+    n = max(0, int(args.settle_s / max(dt, 1e-6)))
+    if n:
+        timed(n)
+    return 1 + n
 
 
 def run_bytes(args, ranks):
@@ -396,6 +423,10 @@ def run_bytes(args, ranks):
                                              H, W, W, 0, H, k, args.strip, slots[i].data_ptr(), stream))
         cur.reverse()
 
+    def steps_n(n):
+        for i in range(n):
+            step(i % slots.shape[0])
+    settle = settle_steps(args, ranks, steps_n, torch_sync=True)
     for i in range(args.warmup):
         step(i)
     # (the count's reduction below is loaded and run once here: a first use inside the timed region
@@ -423,7 +454,8 @@ def run_bytes(args, ranks):
     roof = roofline("bytes", kms, float(H * W * k), pmc, note)
     cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k,
            "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "1gpu",
-           "alive_count_every_step": k > 1, "alive_final": alive, "turns_done": (args.warmup + args.steps) * k}
+           "alive_count_every_step": k > 1, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
+           "settle_steps": settle}
     return value, dt, cfg, roof, "u8 (byte per cell)"
 
 

@@ -192,7 +192,7 @@ def test_bench_share_gpu_shards_over_ipc(G):
         lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
         assert len(lines) == 1, p.stdout[-2000:]
         return json.loads(lines[0])
-    common = ["--width", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    common = ["--width", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--settle-s", "0"]
     two = line(["--gpus", "2", "--share-gpu", "--rows-per-gpu", "2048"] + common)
     one = line(["--rows-per-gpu", "4096"] + common)
     assert two["n_gpus"] == 2 and two["config"]["parallelism"] == "rows2" and two["config"]["transport"] == "ipc"

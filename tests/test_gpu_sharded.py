@@ -156,7 +156,7 @@ def test_bench_self_launch_two_replicas():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    common = ["--workload", "bit64k", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    common = ["--workload", "bit64k", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--settle-s", "0"]
     two = _bench_line(["--gpus", "2", "--share-gpu"] + common)
     one = _bench_line(common)
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
@@ -166,3 +166,18 @@ def test_bench_self_launch_two_replicas():
     k = one["config"]["turns_per_step"]
     assert abs(two["value"] - 2 * 65536 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
     assert one["roofline"]["launch_ms"] > 0 and one["config"]["timed_launches"] == 3
+
+
+def test_bench_settle_steps_reported():
+    """The clock-settle phase (bench.py --settle-s, default 0.3 s): untimed steps before the
+    warmup, reported as config.settle_steps and counted in turns_done; the timed steps are exactly
+    --steps launches."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    line = _bench_line(["--workload", "bit64k", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--settle-s", "0.2"])
+    cfg = line["config"]
+    k = cfg["turns_per_step"]
+    assert cfg["settle_steps"] >= 2  # one timed probe + the rest (a bit64k step is ~1.5 ms)
+    assert cfg["turns_done"] == (cfg["settle_steps"] + 1 + 4) * k
+    assert cfg["timed_launches"] == 4 and line["steps"] == 4 and line["warmup"] == 1
