@@ -43,6 +43,9 @@ VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4  # wave64 VALU instructions/s: 1024 SIMDs 
 BITS_BYTES_PER_UPDATE = 0.25  # 1 bit read + 1 bit written per cell per turn
 BYTES_BYTES_PER_UPDATE = 2.0  # 1 byte read + 1 byte written
 KERNEL_SRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernels.hip")
+# nominal rates of the settle steps (bench.py --settle-s): ~the measured 1-GPU rates
+SETTLE_RATE_BITS = 145e12
+SETTLE_RATE_BYTES = 58e12
 
 
 def parse(argv=None):
@@ -66,10 +69,11 @@ def parse(argv=None):
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle-s", type=float, default=0.3,
-                    help="before the warmup steps, untimed steps of the same workload until the GPU has run "
-                         "this many seconds: the shader clock settles during the first ~0.1-0.2 s of load "
-                         "(DESIGN.md §6), and a short --warmup (the driver's 5 weak steps = 58 ms) left the "
-                         "first timed steps on a lower clock; reported as config.settle_steps (0 = off)")
+                    help="before the warmup steps, untimed steps of the same workload for about this many "
+                         "seconds of GPU work (a fixed count per workload from a nominal rate): the shader clock "
+                         "settles during the first ~0.1-0.2 s of load (DESIGN.md §6), and a short --warmup (the "
+                         "driver's 5 weak steps = 58 ms) left the first timed steps on a lower clock; reported as "
+                         "config.settle_steps (0 = off)")
     ap.add_argument("--snapshot", default="",
                     help="after the timed steps write the board as a P5 file here (every rank its own "
                          "rows, gol_engine_write_pgm: config 5's snapshot); reported, not part of value")
@@ -315,7 +319,8 @@ def run_bits(args, ranks):
     info = e.info()
     k = info["turns_per_launch"]
     e.load_random(1)
-    settle = settle_steps(args, ranks, lambda n: e.step_counted(n * k, k), torch_sync=False)
+    settle = settle_steps(args, lambda n: e.step_counted(n * k, k), float(H // ranks.world if sharded else H) * W * k,
+                          SETTLE_RATE_BITS)
     if args.warmup:
         e.step_counted(args.warmup * k, k)
     ranks.barrier()
@@ -366,25 +371,16 @@ def run_bits(args, ranks):
     return value, dt, cfg, roof, dtype
 
 
-def settle_steps(args, ranks, run_n, torch_sync):
-    """Untimed steps before the warmup until the GPU has been busy for args.settle_s seconds (the
-    shader clock's settling time).  The count comes from one timed step, maxed over
-    the ranks, so every rank runs the same steps (the sharded steps are collective)."""
+def settle_steps(args, run_n, cell_updates_per_step, nominal_rate):
+    """Untimed steps before the warmup for about args.settle_s seconds of GPU work (the shader
+    clock's settling time).  The count comes from a nominal rate (cell-updates/s),
+    not from a clock, so every run and every rank of a workload runs the same turns (the sharded
+    steps are collective, and the final alive count stays reproducible)."""
     if args.settle_s <= 0:
         return 0
-    import torch
-
-    def timed(n):
-        t0 = time.perf_counter()
-        run_n(n)
-        if torch_sync:
-            torch.cuda.synchronize()
-        return time.perf_counter() - t0
-    dt = ranks.max(timed(1))
-    n = max(0, int(args.settle_s / max(dt, 1e-6)))
-    if n:
-        timed(n)
-    return 1 + n
+    n = max(1, int(args.settle_s * nominal_rate / cell_updates_per_step + 0.5))
+    run_n(n)
+    return n
 
 
 def run_bytes(args, ranks):
@@ -426,7 +422,7 @@ def run_bytes(args, ranks):
     def steps_n(n):
         for i in range(n):
             step(i % slots.shape[0])
-    settle = settle_steps(args, ranks, steps_n, torch_sync=True)
+    settle = settle_steps(args, steps_n, float(H) * W * k, SETTLE_RATE_BYTES)
     for i in range(args.warmup):
         step(i)
     # (the count's reduction below is loaded and run once here: a first use inside the timed region

@@ -170,14 +170,15 @@ def test_bench_self_launch_two_replicas():
 
 def test_bench_settle_steps_reported():
     """The clock-settle phase (bench.py --settle-s, default 0.3 s): untimed steps before the
-    warmup, reported as config.settle_steps and counted in turns_done; the timed steps are exactly
-    --steps launches."""
+    warmup, a fixed count per workload (reproducible turns and counts), reported as
+    config.settle_steps and counted in turns_done; the timed steps are exactly --steps launches."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     line = _bench_line(["--workload", "bit64k", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--settle-s", "0.2"])
     cfg = line["config"]
     k = cfg["turns_per_step"]
-    assert cfg["settle_steps"] >= 2  # one timed probe + the rest (a bit64k step is ~1.5 ms)
+    # a fixed count from the nominal rate: 0.2 s x 145e12 / (65536^2 x 12) ~ 562 steps of bit64k
+    assert cfg["settle_steps"] == int(0.2 * 145e12 / (65536 * 65536 * k) + 0.5)
     assert cfg["turns_done"] == (cfg["settle_steps"] + 1 + 4) * k
     assert cfg["timed_launches"] == 4 and line["steps"] == 4 and line["warmup"] == 1
