@@ -37,6 +37,9 @@
 // s_sleep argument between two polls of a pipeline flag (units of 64 shader cycles): 0 (the
 // poll's own LDS round trip paces it) measured +1 % on 65536^2, +0.3 % on 16384^2 bytes, equal on
 // the weak board, over 1; 2 was slower (same box, tools/ab.py)
+#ifndef GOL_BYTES_SPIN_SLEEP
+#define GOL_BYTES_SPIN_SLEEP 0  // (the byte pipeline's polls, spin_until_ge<true>)
+#endif
 #ifndef GOL_SPIN_SLEEP
 #define GOL_SPIN_SLEEP 0
 #endif
@@ -686,7 +689,7 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
             if constexpr (YIELD) __builtin_amdgcn_s_setprio(1);
             return x;
         }
-        __builtin_amdgcn_s_sleep(GOL_SPIN_SLEEP);
+        __builtin_amdgcn_s_sleep(YIELD ? GOL_BYTES_SPIN_SLEEP : GOL_SPIN_SLEEP);
     }
     if constexpr (YIELD) __builtin_amdgcn_s_setprio(1);
     return -1;
