@@ -42,7 +42,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameter
 VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4  # wave64 VALU instructions/s: 1024 SIMDs x 1 per 2 cycles x 2.4 GHz
 BITS_BYTES_PER_UPDATE = 0.25  # 1 bit read + 1 bit written per cell per turn
 BYTES_BYTES_PER_UPDATE = 2.0  # 1 byte read + 1 byte written
-KERNEL_SRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernels.hip")
+# the kernel sources and the flags they are compiled with (a PMC profile is keyed to their hash)
+KERNEL_SRCS = [os.path.join(ROOT, "gol-distributed-final_amd", "csrc", f)
+               for f in ("gol_kernels.hip", "gol_band_pipe.hip", "Makefile")]
 # nominal rates of the settle steps (bench.py --settle-s): ~the measured 1-GPU rates
 SETTLE_RATE_BITS = 145e12
 SETTLE_RATE_BYTES = 58e12
@@ -200,13 +202,17 @@ class Ranks:
 
 # ------------------------------------------------------------------ measurement helpers
 def kernel_source_hash() -> str:
-    with open(KERNEL_SRC, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for path in KERNEL_SRCS:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def load_pmc(key):
     """PMC counters per launch of this workload's step kernel (tools/pmc_summary.py), only if they
-    were measured on the current gol_kernels.hip (sha256 prefix): a stale profile is not used."""
+    were measured on the current kernel sources and build flags (sha256 prefix of gol_kernels.hip,
+    gol_band_pipe.hip and the Makefile): a stale profile is not used."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
@@ -216,7 +222,7 @@ def load_pmc(key):
     if not e:
         return None, "missing"
     if e.get("kernel_src") != kernel_source_hash():
-        return None, "stale (profiled on another gol_kernels.hip)"
+        return None, "stale (profiled on other kernel sources or flags)"
     return e, e.get("profile")
 
 

@@ -1074,6 +1074,47 @@ band_pipe_kernel(BitsArgs a)
     }
 }
 
+#ifdef GOL_TU_BAND_PIPE
+}  // namespace golk
+
+// gol_band_pipe.hip: this file up to here, compiled on its own with the max-ILP machine
+// scheduler (Makefile BANDFLAGS): band_pipe_kernel's instantiations, their host stubs and launch.
+// The scheduler choice is per translation unit, and it is a per-kernel one: same box, 2 reps,
+// max-ILP ran the band boards 1.0-1.9 % faster (weak 148.3 vs 146.8, 262144^2 151.5 vs 148.9,
+// 65536^2 139.8 vs 137.2) and the byte pipeline 4.5 % slower (56.8 vs 59.4);
+// profiles/r04/r04h_sched.jsonl.
+using namespace golk;
+const void *golk_band_pipe_fn(bool contig, bool count, bool rowf)
+{
+    constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
+    if (rowf)
+        return contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true, true> : (const void *)band_pipe_kernel<KW, P, true, false, true>)
+                      : (count ? (const void *)band_pipe_kernel<KW, P, false, true, true> : (const void *)band_pipe_kernel<KW, P, false, false, true>);
+    return contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true> : (const void *)band_pipe_kernel<KW, P, true, false>)
+                  : (count ? (const void *)band_pipe_kernel<KW, P, false, true> : (const void *)band_pipe_kernel<KW, P, false, false>);
+}
+hipError_t golk_band_pipe_launch(bool contig, bool count, bool rowf, unsigned nwg, const BitsArgs &a, hipStream_t s)
+{
+    constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
+    const dim3 g(nwg), blk(64 * P);
+    if (rowf) {
+        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, true>), g, blk, 0, s, a);
+        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, true>), g, blk, 0, s, a);
+        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, true>), g, blk, 0, s, a);
+        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, true>), g, blk, 0, s, a);
+    } else if (contig && count) {
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), g, blk, 0, s, a);
+    } else if (contig) {
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false>), g, blk, 0, s, a);
+    } else if (count) {
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), g, blk, 0, s, a);
+    } else {
+        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false>), g, blk, 0, s, a);
+    }
+    return hipGetLastError();
+}
+#else  // the rest of the kernels and the host side
+
 // 32 x 32 bit-matrix transpose in registers: afterwards x[i] bit b = (before) x[b] bit i.
 __device__ __forceinline__ void transpose32(uint32_t (&x)[32])
 {
@@ -2390,13 +2431,16 @@ static bool band_rank_map(int64_t rows, int64_t ngroups, int64_t pitch, int cus,
     return true;
 }
 
+// band_pipe_kernel lives in its own translation unit (gol_band_pipe.hip: another scheduler)
+const void *golk_band_pipe_fn(bool contig, bool count, bool rowf);
+hipError_t golk_band_pipe_launch(bool contig, bool count, bool rowf, unsigned nwg, const BitsArgs &a, hipStream_t s);
+
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
     constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
     const bool count = a.slots != nullptr;
-    const void *kf = contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true> : (const void *)band_pipe_kernel<KW, P, true, false>)
-                            : (count ? (const void *)band_pipe_kernel<KW, P, false, true> : (const void *)band_pipe_kernel<KW, P, false, false>);
+    const void *kf = golk_band_pipe_fn(contig, count, false);
     // (the row-flag instantiations have the same resources: one occupancy query serves both)
     int64_t nwg = 0;
     const int cus = device_cus();
@@ -2420,25 +2464,11 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
             nwg = a.sm.tail_l + a.ngroups * ((tail_rows + ts - 1) / ts);
         }
     }
-    const dim3 g((unsigned)nwg), blk(64 * P);
 #ifndef GOL_BAND_RANK_ROWF
 #define GOL_BAND_RANK_ROWF 1
 #endif
-    if (a.sm.ranked && GOL_BAND_RANK_ROWF) {  // one-round launch: row-grain hand-off flags
-        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, true>), g, blk, 0, s, a);
-        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, true>), g, blk, 0, s, a);
-        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, true>), g, blk, 0, s, a);
-        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, true>), g, blk, 0, s, a);
-    } else if (contig && count) {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), g, blk, 0, s, a);
-    } else if (contig) {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false>), g, blk, 0, s, a);
-    } else if (count) {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), g, blk, 0, s, a);
-    } else {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false>), g, blk, 0, s, a);
-    }
-    return hipGetLastError();
+    // one-round launch: row-grain hand-off flags
+    return golk_band_pipe_launch(contig, count, a.sm.ranked && GOL_BAND_RANK_ROWF, (unsigned)nwg, a, s);
 }
 
 hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
@@ -2492,7 +2522,7 @@ double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int64_t pitch, int 
 {
     if (!band || dw != 4 || k != 12 || rows <= 0) return 1e9;
     const int64_t ngroups = (Wd + band_useful_words(k, dw) - 1) / band_useful_words(k, dw);
-    const int64_t slots = resident_workgroups((const void *)band_pipe_kernel<GOL_BAND_KW, GOL_BAND_P, true, true>, 64 * GOL_BAND_P);
+    const int64_t slots = resident_workgroups(golk_band_pipe_fn(true, true, false), 64 * GOL_BAND_P);
     if (slots <= 0) return 1e9;
     StripMap sm{};
     if (strip <= 0 && band_rank_map(rows, ngroups, pitch, device_cus(), slots, nullptr, sm)) return 1.0;
@@ -2713,3 +2743,4 @@ hipError_t golk_ipc_wait(const uint32_t *const *flags, int n, uint32_t want, uin
     hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }
+#endif  // GOL_TU_BAND_PIPE

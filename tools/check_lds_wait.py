@@ -25,11 +25,18 @@ CSRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
 
 
 def compile_asm(out):
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                    "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",  # as the Makefile's KFLAGS
-                    "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "--cuda-device-only", "-S",
-                    os.path.join(CSRC, "gol_kernels.hip"), "-o", out], check=True,
-                   stderr=subprocess.DEVNULL)
+    """Both kernel translation units with the Makefile's flags (KFLAGS; gol_band_pipe.hip also
+    BANDFLAGS, the max-ILP scheduler), concatenated into one assembly file."""
+    parts = []
+    for src, extra in (("gol_kernels.hip", []), ("gol_band_pipe.hip", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"])):
+        part = out + "." + src + ".s"
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                        "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"] + extra +  # as the Makefile
+                       ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "--cuda-device-only", "-S",
+                        os.path.join(CSRC, src), "-o", part], check=True, stderr=subprocess.DEVNULL)
+        parts.append(open(part).read())
+    with open(out, "w") as f:
+        f.write("\n".join(parts))
 
 
 def regs(text):

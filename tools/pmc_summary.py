@@ -80,8 +80,9 @@ if not out:
 main = max(out, key=lambda k: stats.get(k, {}).get("TotalNs", 0))
 tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 t = json.load(open(tp)) if os.path.exists(tp) else {}
-src_hash = hashlib.sha256(open(os.path.join(ROOT, "gol-distributed-final_amd", "csrc", "gol_kernels.hip"),
-                                "rb").read()).hexdigest()[:16]
+sys.path.insert(0, ROOT)
+from bench import kernel_source_hash  # noqa: E402  (the kernel sources + Makefile, as bench.py checks)
+src_hash = kernel_source_hash()
 if "hbm_bytes_per_launch" in out[main]:
     t[key] = {"kernel": main, "kernel_src": src_hash, "trace_calls": stats[main]["Calls"], "bytes_per_launch": out[main]["hbm_bytes_per_launch"],
               "profile": f"profiles/{tag}", "avg_ns_trace": out[main]["avg_ns_trace"]}

@@ -80,7 +80,7 @@ def build(flags=""):
         src = src[:k] + STORE + src[k + len(COUNT_LINE):]
     open(os.path.join(OUT, "gol_kernels.hip"), "w").write(src)
     for f in os.listdir(CSRC):
-        if f.endswith((".cpp", ".h")) or f == "Makefile":
+        if f.endswith((".cpp", ".h")) or f == "Makefile" or (f.endswith(".hip") and f != "gol_kernels.hip"):
             with open(os.path.join(CSRC, f)) as a, open(os.path.join(OUT, f), "w") as b:
                 b.write(a.read())
     subprocess.run(["make", "-s", "-j8", "-C", OUT, "ARCH=gfx950", "BUILD=./obj", "OUT=./libtimeline.so",
