@@ -44,7 +44,7 @@ BITS_BYTES_PER_UPDATE = 0.25  # 1 bit read + 1 bit written per cell per turn (SU
 BYTES_BYTES_PER_UPDATE = 2.0  # 1 byte read + 1 byte written
 # the kernel sources and the flags they are compiled with (a PMC profile is keyed to their hash)
 KERNEL_SRCS = [os.path.join(ROOT, "gol-distributed-final_amd", "csrc", f)
-               for f in ("gol_kernels.hip", "gol_band_pipe.hip", "Makefile")]
+               for f in ("gol_kernels.hip", "gol_band_pipe.hip", "gol_bytes_pipe.hip", "Makefile")]
 # nominal rates of the settle steps (bench.py --settle-s): ~the measured 1-GPU rates
 SETTLE_RATE_BITS = 145e12
 SETTLE_RATE_BYTES = 58e12
@@ -212,7 +212,7 @@ def kernel_source_hash() -> str:
 def load_pmc(key):
     """PMC counters per launch of this workload's step kernel (tools/pmc_summary.py), only if they
     were measured on the current kernel sources and build flags (sha256 prefix of gol_kernels.hip,
-    gol_band_pipe.hip and the Makefile): a stale profile is not used."""
+    gol_band_pipe.hip, gol_bytes_pipe.hip and the Makefile): a stale profile is not used."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:

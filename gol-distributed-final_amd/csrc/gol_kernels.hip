@@ -1648,6 +1648,32 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     if (COUNT && wv == P - 1) slot_add(a.slots, alive);
 }
 
+#ifndef GOL_BYTES_PIPE_STAGES
+#define GOL_BYTES_PIPE_STAGES 4, 4, 4
+#define GOL_BYTES_PIPE_P 8
+#endif
+#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
+
+#ifdef GOL_TU_BYTES_PIPE
+}  // namespace golk
+
+// gol_bytes_pipe.hip: this file up to here, compiled on its own with the max-memory-clause
+// machine scheduler (Makefile BYTEFLAGS): bytes_pipe_kernel's instantiations and launch.  Same
+// box, 3 reps: 59.4 -> 60.4 TCUPS on 16384^2 bytes; under max-ILP (the band pipeline's) 56.8
+// (profiles/r04/r04h_sched.jsonl).
+using namespace golk;
+const void *golk_bytes_pipe_fn(bool count)
+{
+    return count ? (const void *)BYTES_PIPE(true) : (const void *)BYTES_PIPE(false);
+}
+hipError_t golk_bytes_pipe_launch(bool count, unsigned nwg, const BytesKArgs &a, hipStream_t s)
+{
+    if (count) hipLaunchKernelGGL(BYTES_PIPE(true), dim3(nwg), dim3(64 * GOL_BYTES_PIPE_P), 0, s, a);
+    else hipLaunchKernelGGL(BYTES_PIPE(false), dim3(nwg), dim3(64 * GOL_BYTES_PIPE_P), 0, s, a);
+    return hipGetLastError();
+}
+#else  // the rest of the kernels and the host side
+
 // ------------------------------------------------------------------ byte-board step (exact semantics)
 // SWAR on 4 cells per uint32.  A = (byte == 255), Z = (byte == 0), as 0x01 per byte.
 __device__ __forceinline__ uint32_t bytes_eq_ff(uint32_t d)
@@ -2393,11 +2419,9 @@ static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 #ifndef GOL_BYTES_PAIRED
 #define GOL_BYTES_PAIRED 1
 #endif
-#ifndef GOL_BYTES_PIPE_STAGES
-#define GOL_BYTES_PIPE_STAGES 4, 4, 4
-#define GOL_BYTES_PIPE_P 8
-#endif
-#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
+// bytes_pipe_kernel lives in its own translation unit (gol_bytes_pipe.hip: another scheduler)
+const void *golk_bytes_pipe_fn(bool count);
+hipError_t golk_bytes_pipe_launch(bool count, unsigned nwg, const BytesKArgs &a, hipStream_t s);
 // Rows per strip of the band pipeline's launches of many rounds (same box, weak board, 3 reps:
 // 1024 148.4 TCUPS, 2048 148.3, 4096 147.0; profiles/r04/r04d_ab_rounds.jsonl)
 #ifndef GOL_BAND_STRIP
@@ -2587,7 +2611,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         // one workgroup of GOL_BYTES_PIPE_P waves per (column group, strip): rank-weighted strips
         // in one round, else round-tiled strips >= 4k rows
         const bool count = a.slots != nullptr;
-        const void *kf = count ? (const void *)BYTES_PIPE(true) : (const void *)BYTES_PIPE(false);
+        const void *kf = golk_bytes_pipe_fn(count);
         const int cus = device_cus();
         const int64_t slots = resident_workgroups(kf, 64 * BYTES_PIPE_P);
         int64_t nwg = 0;
@@ -2607,9 +2631,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
             a.strip = (int)std::min<int64_t>(a.strip, max_rows);
             nwg = (int64_t)a.ngroups * ((rows + a.strip - 1) / a.strip);
         }
-        if (count) hipLaunchKernelGGL(BYTES_PIPE(true), dim3((unsigned)nwg), dim3(64 * BYTES_PIPE_P), 0, s, a);
-        else hipLaunchKernelGGL(BYTES_PIPE(false), dim3((unsigned)nwg), dim3(64 * BYTES_PIPE_P), 0, s, a);
-        return hipGetLastError();
+        return golk_bytes_pipe_launch(count, (unsigned)nwg, a, s);
     }
     const int nstrips = (int)((rows + a.strip - 1) / a.strip);
     dim3 grid((a.ngroups + 3) / 4, nstrips);
@@ -2744,3 +2766,4 @@ hipError_t golk_ipc_wait(const uint32_t *const *flags, int n, uint32_t want, uin
     return hipGetLastError();
 }
 #endif  // GOL_TU_BAND_PIPE
+#endif  // GOL_TU_BYTES_PIPE

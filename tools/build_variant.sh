@@ -8,9 +8,9 @@ N=$1; F=$2
 D=$R/tools/variants/src_$N
 rm -rf "$D" && mkdir -p "$D"
 cp "$R"/gol-distributed-final_amd/csrc/{Makefile,*.cpp,*.h,*.hip} "$D/"
-# (environment BANDFLAGS / KFLAGS, if set, replace the Makefile's scheduler / kernel flags)
+# (environment BANDFLAGS / BYTEFLAGS / KFLAGS, if set, replace the Makefile's scheduler / kernel flags)
 make -s -j8 -C "$D" ARCH=gfx950 BUILD=./obj OUT=../lib$N.so INC=$R/include \
     CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -I$R/include -I. $F" \
-    ${BANDFLAGS+BANDFLAGS="$BANDFLAGS"} ${KFLAGS+KFLAGS="$KFLAGS"}
+    ${BANDFLAGS+BANDFLAGS="$BANDFLAGS"} ${BYTEFLAGS+BYTEFLAGS="$BYTEFLAGS"} ${KFLAGS+KFLAGS="$KFLAGS"}
 rm -rf "$D"  # (the copied sources are not needed once built)
 echo "$R/tools/variants/lib$N.so"

@@ -25,10 +25,13 @@ CSRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
 
 
 def compile_asm(out):
-    """Both kernel translation units with the Makefile's flags (KFLAGS; gol_band_pipe.hip also
-    BANDFLAGS, the max-ILP scheduler), concatenated into one assembly file."""
+    """The kernel translation units with the Makefile's flags (KFLAGS; the pipeline units also
+    BANDFLAGS / BYTEFLAGS, their schedulers), concatenated into one assembly file."""
     parts = []
-    for src, extra in (("gol_kernels.hip", []), ("gol_band_pipe.hip", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"])):
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    flags = {v: re.search(r"^%s = (.*)$" % v, mk, re.M).group(1).split() for v in ("BANDFLAGS", "BYTEFLAGS")}
+    for src, extra in (("gol_kernels.hip", []), ("gol_band_pipe.hip", flags["BANDFLAGS"]),
+                       ("gol_bytes_pipe.hip", flags["BYTEFLAGS"])):
         part = out + "." + src + ".s"
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                         "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"] + extra +  # as the Makefile
