@@ -70,7 +70,7 @@ def parse(argv=None):
     ap.add_argument("--rows-per-gpu", type=int, default=1 << 17)
     ap.add_argument("--width", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--settle-s", type=float, default=0.3,
+    ap.add_argument("--settle-s", type=float, default=0.6,
                     help="before the warmup steps, untimed steps of the same workload for about this many "
                          "seconds of GPU work (a fixed count per workload from a nominal rate): the shader clock "
                          "settles during the first ~0.1-0.2 s of load (DESIGN.md §6), and a short --warmup (the "
