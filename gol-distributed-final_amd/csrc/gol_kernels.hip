@@ -1658,10 +1658,10 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
 }  // namespace golk
 
 // gol_bytes_pipe.hip: this file up to here, compiled on its own with the max-memory-clause
-// machine scheduler and no post-RA scheduler (Makefile BYTEFLAGS): bytes_pipe_kernel's
-// instantiations and launch.  Same box, 3 reps: 59.4 -> 60.4 TCUPS on 16384^2 bytes, then
-// 60.2 -> 60.6 without the post-RA pass; under max-ILP (the band pipeline's) 56.8
-// (profiles/r04/r04h_sched.jsonl).
+// machine scheduler, bottom-up, and no post-RA scheduler (Makefile BYTEFLAGS): bytes_pipe_kernel's
+// instantiations and launch.  Same box, 3 reps each: 59.4 -> 60.4 TCUPS on 16384^2 bytes, then
+// 60.2 -> 60.6 without the post-RA pass, 60.7 -> 61.2 bottom-up; under max-ILP (the band
+// pipeline's) 56.8 (profiles/r04/r04h_sched.jsonl).
 using namespace golk;
 const void *golk_bytes_pipe_fn(bool count)
 {
