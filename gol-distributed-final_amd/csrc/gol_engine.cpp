@@ -47,6 +47,13 @@
     } while (0)
 
 static constexpr size_t SLOT_BYTES = GOL_COUNT_SLOTS * 8 * sizeof(uint64_t);
+// The count points of a stepping call: the launch that ends point ci adds its cells into slot
+// array 1 + ci % GOL_SLOT_BATCH, and one reduce kernel sums a run of such arrays into counts[]
+// (flush_counts); array 0 serves single counts (count_into_slots, hash).  Against a reduce per
+// point: 65536^2 139.5 -> 140.3 TCUPS, the big boards +0.3 % (same box, 3 reps, same counts;
+// profiles/r04/r04l_count_batch.jsonl).
+#define GOL_SLOT_BATCH 64
+static constexpr size_t SLOT_WORDS = GOL_COUNT_SLOTS * 8;
 
 static int set_dev(int d)
 {
@@ -134,7 +141,7 @@ static int shard_alloc(gol_engine *e, gol_shard &s)
     golk_own_stream(s.stream);
     golk_own_stream(s.edge);
     for (hipEvent_t *ev : {&s.ev_start, &s.ev_edge, &s.ev_halo}) HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&s.slots, SLOT_BYTES));
+    HIPCHK(hipMalloc(&s.slots, SLOT_BYTES * (1 + GOL_SLOT_BATCH)));
     HIPCHK(hipMalloc(&s.flag, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&s.err, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&s.coll, GOL_COLL_WORDS * sizeof(uint32_t)));
@@ -385,6 +392,7 @@ static int sync_all(gol_engine *e, bool collective = true)
             RCCHK(set_dev(s.device));
             HIPCHK(hipMemsetAsync(s.err, 0, sizeof(uint32_t), s.stream));
             s.slots_zero = false;  // a faulted launch may have left counts in them
+            s.batch_zero = false;
             // a timed-out pair may have left its claims set: this engine's streams only
             HIPCHK(golk_reset_claims(s.stream));
             HIPCHK(golk_reset_claims(s.edge));
@@ -756,8 +764,38 @@ static int step_mode(gol_engine *e, const gol_shard &s, int k)
 // on the edge stream and the interior beside them on the compute stream; the next step's halo
 // exchange starts as soon as the edge rows are written, while the interior is still running.
 // With `count` the alive cells of the output are added to each shard's slots.
-static int launch_k(gol_engine *e, int k, bool count)
+static uint64_t *batch_slots(gol_shard &s, int64_t ci) { return s.slots + (1 + ci % GOL_SLOT_BATCH) * SLOT_WORDS; }
+
+// Reduce the pending count points' slot arrays into counts[pend_first, pend_first + pend_n) (the
+// reduce leaves them zeroed).
+static int flush_counts(gol_engine *e)
 {
+    if (e->pend_n == 0) return GOL_OK;
+    for (auto &s : e->sh) {
+        RCCHK(set_dev(s.device));
+        HIPCHK(golk_slots_reduce(batch_slots(s, e->pend_first), e->pend_n, s.counts + e->pend_first, s.stream));
+    }
+    e->pend_n = 0;
+    return GOL_OK;
+}
+
+// Before the counted launch of point ci: the pending run must stay contiguous in the arrays, and
+// after a fault every array is zeroed again.
+static int batch_begin(gol_engine *e, int64_t ci)
+{
+    if (e->pend_n && (e->pend_first + e->pend_n != ci || ci % GOL_SLOT_BATCH == 0)) RCCHK(flush_counts(e));
+    for (auto &s : e->sh) {
+        if (s.batch_zero) continue;
+        RCCHK(set_dev(s.device));
+        HIPCHK(hipMemsetAsync(s.slots + SLOT_WORDS, 0, SLOT_BYTES * GOL_SLOT_BATCH, s.stream));
+        s.batch_zero = true;
+    }
+    return GOL_OK;
+}
+
+static int launch_k(gol_engine *e, int k, int64_t count_ci)
+{
+    const bool count = count_ci >= 0;
     if (k > e->kx) return gol_set_error(GOL_EINVAL, "k %d > the exchanged halo (%d rows)", k, e->kx);
     if (!e->halo_ok) RCCHK(exchange_current(e));
     const int n = (int)e->sh.size();
@@ -770,9 +808,7 @@ static int launch_k(gol_engine *e, int k, bool count)
         const int mode = step_mode(e, s, k);
         serial &= mode == GOL_STEP_SERIAL;
         RCCHK(gol_step_plan(s.R, k, e->kx, mode, plan, 3, &np));
-        uint64_t *slots = count ? s.slots : nullptr;
-        if (count && !s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
-        if (count) s.slots_zero = false;
+        uint64_t *slots = count ? batch_slots(s, count_ci) : nullptr;  // (zeroed: batch_begin)
         if (timing_open(e)) e->tcall_cells[i] += (double)s.R * (double)e->W * k;
         HIPCHK(hipEventRecord(s.ev_start, s.stream));  // the step's inputs are complete, slots zeroed
         bool edge_used = false, waited[2] = {false, false};
@@ -863,10 +899,10 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
                 // 0/255 byte board: k turns per launch on the bytes (torus wrap through top/bot)
                 const int k = e->k >= 32 && n >= 32 && e->H >= 32 ? 32 : pick_k(e->k, n, e->H, 1, false);
                 const bool last = n == k && ci >= 0;
-                if (last && !s.slots_zero) HIPCHK(hipMemsetAsync(s.slots, 0, SLOT_BYTES, s.stream));
-                if (last) s.slots_zero = false;
+                if (last) RCCHK(batch_begin(e, ci));
                 HIPCHK(golk_bytes_blocked(mid + (e->H - k) * e->bstride, mid, mid, s.bytes[1 - e->bcur], e->H, e->W,
-                                          e->bstride, 0, e->H, k, e->strip, last ? s.slots : nullptr, s.err, s.stream));
+                                          e->bstride, 0, e->H, k, e->strip, last ? batch_slots(s, ci) : nullptr, s.err,
+                                          s.stream));
                 e->bcur = 1 - e->bcur;
                 e->turn += k;
                 n -= k;
@@ -883,13 +919,18 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
         if (e->band_capable) RCCHK(convert(e, true));
         const int k = pick_k(e->k, n, e->min_rows, e->band ? e->band_dw : e->dw, e->band);
         const bool last = n == k && ci >= 0;
-        RCCHK(launch_k(e, k, last));
+        if (last) RCCHK(batch_begin(e, ci));
+        RCCHK(launch_k(e, k, last ? ci : -1));
         e->turn += k;
         n -= k;
         counted = last;
     }
-    if (ci >= 0) {
-        if (!counted) RCCHK(count_into_slots(e));
+    if (ci >= 0 && counted) {  // reduced with its run (flush_counts)
+        if (e->pend_n == 0) e->pend_first = ci;
+        ++e->pend_n;
+    } else if (ci >= 0) {
+        RCCHK(flush_counts(e));
+        RCCHK(count_into_slots(e));
         for (auto &s : e->sh) {
             RCCHK(set_dev(s.device));
             HIPCHK(golk_slots_reduce(s.slots, 1, s.counts + ci, s.stream));
@@ -944,6 +985,7 @@ extern "C" int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t eve
         RCCHK(ensure_counts(s, n));
     }
     RCCHK(agree_step_state(e));
+    e->pend_n = 0;
     int rc = timing_begin(e);
     int64_t left = turns, ci = 0;
     while (left > 0 && rc == GOL_OK) {
@@ -951,6 +993,11 @@ extern "C" int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t eve
         rc = advance(e, seg, seg == every ? ci : -1);
         if (seg == every) ++ci;
         left -= seg;
+    }
+    if (rc == GOL_OK) rc = flush_counts(e);
+    if (rc != GOL_OK && e->pend_n) {  // (arrays of points never reduced: zeroed before the next use)
+        e->pend_n = 0;
+        for (auto &s : e->sh) s.batch_zero = false;
     }
     if (rc == GOL_OK) rc = timing_end(e);
     if (rc != GOL_OK) {
@@ -1373,7 +1420,7 @@ extern "C" int gol_engine_step_flips(gol_engine *e, int32_t *xy, int64_t cap, in
     int64_t total = 0;
     if (e->mode == GOL_MODE_BITS) {
         // one standard-layout turn; the previous generation stays in the other buffer
-        RCCHK(launch_k(e, 1, false));
+        RCCHK(launch_k(e, 1, -1));
         e->turn += 1;
         RCCHK(sync_all(e));
         for (auto &s : e->sh) {

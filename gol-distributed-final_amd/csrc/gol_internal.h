@@ -49,8 +49,9 @@ struct gol_shard {
     // BYTES mode: the H x W byte board (double buffer).  EXACT mode: bytes[0] = rows
     // y0-1 .. y1 (R + 2 rows, the halo rows from the host board), bytes[1] = R output rows.
     uint8_t *bytes[2] = {nullptr, nullptr};
-    uint64_t *slots = nullptr;        // GOL_COUNT_SLOTS * 8 reduction slots
-    bool slots_zero = false;          // zeroed by the last slots reduce (no memset before the next count)
+    uint64_t *slots = nullptr;        // 1 + GOL_SLOT_BATCH arrays of GOL_COUNT_SLOTS * 8 reduction slots
+    bool slots_zero = false;          // array 0 zeroed by the last slots reduce (no memset before the next count)
+    bool batch_zero = false;          // arrays 1.. zero except those of pending count points (flush_counts)
     uint64_t *counts = nullptr;       // per-count-point alive counts (step_counted)
     int64_t counts_cap = 0;
     uint32_t *flag = nullptr;         // nonbinary flag of a load
@@ -110,6 +111,7 @@ struct gol_engine {
     bool halo_ok = false;      // the ghost rows of bits[cur] hold the current halo (kx rows)
     bool halo_issued = false;  // an exchange was enqueued since the last synchronisation point
     bool halo_on_compute = false;  // the last exchange ran on the compute streams (RCCL after a SERIAL step)
+    int64_t pend_first = 0, pend_n = 0;  // count points whose slot arrays await one reduce (flush_counts)
     bool timing = false;
     std::vector<gol_timed> timed;
     std::vector<size_t> tcall_ev;      // the current stepping call's start events (one per shard)
