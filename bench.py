@@ -463,6 +463,9 @@ def run_bytes(args, ranks):
 
 def main():
     args = parse()
+    if os.environ.get("GOL_BENCH_STACKS_AFTER_S"):  # debugging a stuck run: every thread's stack to stderr
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GOL_BENCH_STACKS_AFTER_S"]), repeat=True)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     if args.k <= 0 and args.workload == "byte16k":

@@ -54,6 +54,8 @@ static constexpr size_t SLOT_BYTES = GOL_COUNT_SLOTS * 8 * sizeof(uint64_t);
 // profiles/r04/r04l_count_batch.jsonl).
 #define GOL_SLOT_BATCH 64
 static constexpr size_t SLOT_WORDS = GOL_COUNT_SLOTS * 8;
+// The IPC transport's send buffer (exchange_ipc): 2 exchange parities x 4 plan ops x the ghost rows.
+static size_t ipc_out_bytes(const gol_engine *e) { return (size_t)2 * 4 * GOL_GHOST_ROWS * e->pitch * sizeof(uint32_t); }
 
 static int set_dev(int d)
 {
@@ -123,6 +125,7 @@ static void shard_release(gol_shard &s)
     if (s.flag) (void)hipFree(s.flag);
     if (s.err) (void)hipFree(s.err);
     if (s.coll) (void)hipFree(s.coll);
+    if (s.ipc_out) (void)hipFree(s.ipc_out);
     if (s.host_word) (void)hipHostFree(s.host_word);
     if (s.staging) (void)hipFree(s.staging);
     if (s.host_staging) (void)hipHostFree(s.host_staging);
@@ -313,8 +316,15 @@ extern "C" int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int3
             if (p != rank && std::find(e->ipc_peers.begin(), e->ipc_peers.end(), p) == e->ipc_peers.end())
                 e->ipc_peers.push_back(p);
         rc = set_dev(dev);
-        if (rc == GOL_OK)
-            rc = gol_ipc::open(id, nranks, rank, dev, H, W, e->sh[0].bits_alloc, e->ipc_peers, &e->ipc);
+        // the peers pull from a small send buffer, not from the board: importing whole boards
+        // (2 GiB each for config 4 over 4 ranks) hung inside the runtime's IPC import
+        gol_shard &s0 = e->sh[0];
+        const size_t ob = ipc_out_bytes(e);
+        if (rc == GOL_OK && hipMalloc(&s0.ipc_out, ob) != hipSuccess) rc = gol_set_error(GOL_EHIP, "IPC send rows: hipMalloc failed");
+        if (rc == GOL_OK && (hipMemset(s0.ipc_out, 0, ob) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+            rc = gol_set_error(GOL_EHIP, "IPC send rows: hipMemset failed");
+        uint32_t *const bufs[2] = {s0.ipc_out, nullptr};
+        if (rc == GOL_OK) rc = gol_ipc::open(id, nranks, rank, dev, H, W, bufs, e->ipc_peers, &e->ipc);
         e->comm = e->ipc;
     }
     if (rc != GOL_OK) {
@@ -516,27 +526,35 @@ static bool local_wrap(const gol_engine *e)
 }
 
 // IPC transport (one shard per process): this rank's exchange xn on its comm stream, pulling
-// each ghost block out of the neighbour's HBM:
-//   1. signal READY = xn once the rows this rank sends are written (ev_edge);
-//   2. wait until each neighbour's READY has reached xn (its rows for this exchange are written);
-//   3. copy every receive of my gol_halo_plan from the peer's matching send (the peer's nth send
-//      to me for my nth receive from it: the pairing RCCL applies to the same plans);
+// each ghost block out of the neighbour's send buffer (ipc_out, mapped by the peers):
+//   1. once the rows this rank sends are written (ev_edge), copy every send of my gol_halo_plan
+//      into ipc_out slot (xn & 1, op index), then signal READY = xn;
+//   2. wait until each neighbour's READY has reached xn (its send rows for this exchange are in);
+//   3. copy every receive of my gol_halo_plan from the peer's matching send slot (the peer's nth
+//      send to me for my nth receive from it: the pairing RCCL applies to the same plans);
 //   4. signal PULLED = xn.
-// A neighbour overwrites the rows it sent only in a later step's halo-reading launch, which
-// waits for its own exchange xn+1, i.e. for my READY xn+1, which I signal after my step's
-// halo-reading launches, which waited for my pulls of xn: so nothing else orders my copies
-// against its writes.  Writes outside a step wait for PULLED explicitly (invalidate_halo).
+// A neighbour overwrites send slot (xn & 1) only at its exchange xn+2, which follows its step
+// after exchange xn+1, which waited for my READY xn+1, which I signal after my step's
+// halo-reading launch, which waited for my pulls of xn: so nothing else orders my copies against
+// its writes.  Writes of the board outside a step wait for PULLED (invalidate_halo).
 static int exchange_ipc(gol_engine *e)
 {
     gol_shard &s = e->sh[0];
     RCCHK(set_dev(s.device));
     const int c = e->cur;
     const int64_t P = e->pitch;
-    const size_t hb = (size_t)e->kx * P * sizeof(uint32_t);
     gol_halo_op mine[4];
     RCCHK(plan_of(e, 0, mine));
     const uint32_t xn = ++e->xn;
+    const int64_t slot_words = (int64_t)GOL_GHOST_ROWS * P;
+    auto out_slot = [&](uint32_t *base, int m) { return base + ((int64_t)(xn & 1) * 4 + m) * slot_words; };
     HIPCHK(hipStreamWaitEvent(s.comm, s.ev_edge, 0));
+    for (int m = 0; m < 4; ++m)
+        if (mine[m].kind == GOL_HALO_SEND) {
+            if (mine[m].rows > GOL_GHOST_ROWS) return gol_set_error(GOL_EINVAL, "halo plan: %d rows per send", mine[m].rows);
+            HIPCHK(hipMemcpyAsync(out_slot(s.ipc_out, m), s.bits[c] + mine[m].row * P, (size_t)mine[m].rows * P * sizeof(uint32_t),
+                                  hipMemcpyDeviceToDevice, s.comm));
+        }
     RCCHK(e->ipc->signal(s.comm, GOL_IPC_READY, xn));
     RCCHK(e->ipc->wait(s.comm, e->ipc_peers, GOL_IPC_READY, xn, s.err));
     for (int j = 0; j < 4; ++j) {
@@ -547,19 +565,14 @@ static int exchange_ipc(gol_engine *e)
         gol_halo_op theirs[4];
         int32_t n = 0;
         RCCHK(gol_halo_plan(e->H, e->nranks, rv.peer, e->kx, theirs, 4, &n));
-        const gol_halo_op *sd = nullptr;  // the peer's nth send to me
-        for (int m = 0, cnt = 0; m < n && !sd; ++m)
-            if (theirs[m].kind == GOL_HALO_SEND && theirs[m].peer == e->rank && cnt++ == nth) sd = &theirs[m];
-        if (!sd || sd->rows != rv.rows) return gol_set_error(GOL_EINVAL, "halo plan: unmatched receive");
-        const uint32_t *src;
-        if (rv.peer == e->rank) {
-            src = s.bits[c];
-        } else {
-            const uint32_t *base = e->ipc->peer_buf(rv.peer, c);
-            if (!base) return gol_set_error(GOL_ESTATE, "IPC: rank %d is not mapped", rv.peer);
-            src = base + (int64_t)GOL_GHOST_ROWS * P;  // row 0 of the peer's buffer
-        }
-        HIPCHK(hipMemcpyAsync(s.bits[c] + rv.row * P, src + sd->row * P, hb, hipMemcpyDeviceToDevice, s.comm));
+        int sm = -1;  // the peer's nth send to me (its op index)
+        for (int m = 0, cnt = 0; m < n && sm < 0; ++m)
+            if (theirs[m].kind == GOL_HALO_SEND && theirs[m].peer == e->rank && cnt++ == nth) sm = m;
+        if (sm < 0 || theirs[sm].rows != rv.rows) return gol_set_error(GOL_EINVAL, "halo plan: unmatched receive");
+        uint32_t *base = rv.peer == e->rank ? s.ipc_out : e->ipc->peer_buf(rv.peer, 0);
+        if (!base) return gol_set_error(GOL_ESTATE, "IPC: rank %d is not mapped", rv.peer);
+        HIPCHK(hipMemcpyAsync(s.bits[c] + rv.row * P, out_slot(base, sm), (size_t)rv.rows * P * sizeof(uint32_t),
+                              hipMemcpyDeviceToDevice, s.comm));
     }
     RCCHK(e->ipc->signal(s.comm, GOL_IPC_PULLED, xn));
     HIPCHK(hipEventRecord(s.ev_halo, s.comm));

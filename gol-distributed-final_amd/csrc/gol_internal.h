@@ -57,6 +57,7 @@ struct gol_shard {
     uint32_t *flag = nullptr;         // nonbinary flag of a load
     uint32_t *err = nullptr;          // device error word of this shard's launches
     uint32_t *coll = nullptr;         // GOL_COLL_WORDS device words for collectives (agreement, barriers)
+    uint32_t *ipc_out = nullptr;      // IPC transport: the rows this rank sends, 2 x 4 x GOL_GHOST_ROWS rows (exchange_ipc)
     uint32_t *host_word = nullptr;    // GOL_HOST_WORDS pinned words: readback of err / flag, collectives
     uint8_t *staging = nullptr;       // device byte rows for chunked copies
     uint8_t *host_staging = nullptr;  // pinned host rows

@@ -230,6 +230,30 @@ static int hip_fail(hipError_t e, const char *what)
     return gol_set_error(e == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 
+// GOL_IPC_TRACE=1: every step of the join on stderr (a rank that hangs in the HIP runtime shows
+// where: the host collectives time out by themselves, runtime calls do not)
+static bool ipc_trace()
+{
+    static const bool on = getenv("GOL_IPC_TRACE") && atoi(getenv("GOL_IPC_TRACE")) > 0;
+    return on;
+}
+#define IPC_TRACE(...)                                                                                  \
+    do {                                                                                                \
+        if (ipc_trace()) {                                                                              \
+            fprintf(stderr, "[golhip ipc r%d %.3f] ", rank,                                             \
+                    std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count()); \
+            fprintf(stderr, __VA_ARGS__);                                                               \
+            fputc('\n', stderr);                                                                        \
+        }                                                                                               \
+    } while (0)
+
+// Ranks open their peers' handles one rank at a time (a host barrier between turns): 4 ranks
+// importing each other's 2 GiB buffers at once hung inside the runtime (config 4's board over 4
+// ranks on one GPU, round 4); 2 ranks and small buffers did not.
+#ifndef GOL_IPC_SERIAL_OPEN
+#define GOL_IPC_SERIAL_OPEN 1
+#endif
+
 int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H, int64_t W, uint32_t *const bufs[2],
                   const std::vector<int> &peers, gol_ipc **out)
 {
@@ -275,10 +299,12 @@ int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H
     if (!s->slot[rank].claimed.compare_exchange_strong(unclaimed, 1u))
         return fail(gol_set_error(GOL_EINVAL, "IPC rank %d joined twice", rank));
 
+    IPC_TRACE("joined the segment %s", name);
     hipError_t he = hipMalloc(&c->flags_, GOL_IPC_FLAG_WORDS * sizeof(uint32_t));
     if (he == hipSuccess) he = hipMemset(c->flags_, 0, GOL_IPC_FLAG_WORDS * sizeof(uint32_t));
     if (he == hipSuccess) he = hipDeviceSynchronize();
     if (he != hipSuccess) return fail(hip_fail(he, "IPC flag words"));
+    IPC_TRACE("flag words allocated");
     gol_ipc_slot &me = s->slot[rank];
     me.pid = (int32_t)getpid();
     me.device = device;
@@ -287,32 +313,51 @@ int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H
     if (he == hipSuccess) he = hipIpcGetMemHandle(&me.flags, c->flags_);
     if (he != hipSuccess) return fail(hip_fail(he, "hipIpcGetMemHandle"));
     me.published.store(1, std::memory_order_release);
+    IPC_TRACE("handles published");
 
     rc = c->host_barrier();  // every rank has published its handles
     if (rc) return fail(rc);
     if (rank == 0) shm_unlink(name);  // mapped by every rank: the name is no longer needed
+    IPC_TRACE("all ranks published");
 
-    for (int r : peers) {
-        if (r == rank || r < 0 || r >= nranks) continue;
-        const gol_ipc_slot &ps = s->slot[r];
-        if (!ps.published.load(std::memory_order_acquire)) return fail(gol_set_error(GOL_ECOMM, "IPC rank %d has no handles", r));
-        if (ps.device != device) {  // (ranks on distinct GPUs: peer access for the pulls and the flag polls)
-            (void)hipDeviceEnablePeerAccess(ps.device, 0);
-            (void)hipGetLastError();
+    auto open_peers = [&]() -> int {
+        for (int r : peers) {
+            if (r == rank || r < 0 || r >= nranks) continue;
+            const gol_ipc_slot &ps = s->slot[r];
+            if (!ps.published.load(std::memory_order_acquire)) return gol_set_error(GOL_ECOMM, "IPC rank %d has no handles", r);
+            if (ps.device != device) {  // (ranks on distinct GPUs: peer access for the pulls and the flag polls)
+                (void)hipDeviceEnablePeerAccess(ps.device, 0);
+                (void)hipGetLastError();
+            }
+            Peer p;
+            p.rank = r;
+            void *q = nullptr;
+            for (int i = 0; i < 2 && he == hipSuccess; ++i) {
+                if (!bufs[i]) continue;
+                IPC_TRACE("opening rank %d's buffer %d", r, i);
+                he = hipIpcOpenMemHandle(&q, ps.buf[i], hipIpcMemLazyEnablePeerAccess);
+                if (he == hipSuccess) p.buf[i] = static_cast<uint32_t *>(q);
+            }
+            IPC_TRACE("opening rank %d's flag words", r);
+            if (he == hipSuccess) he = hipIpcOpenMemHandle(&q, ps.flags, hipIpcMemLazyEnablePeerAccess);
+            if (he == hipSuccess) p.flags = static_cast<uint32_t *>(q);
+            c->peers_.push_back(p);
+            if (he != hipSuccess) return hip_fail(he, "hipIpcOpenMemHandle");
         }
-        Peer p;
-        p.rank = r;
-        void *q = nullptr;
-        for (int i = 0; i < 2 && he == hipSuccess; ++i) {
-            if (!bufs[i]) continue;
-            he = hipIpcOpenMemHandle(&q, ps.buf[i], hipIpcMemLazyEnablePeerAccess);
-            if (he == hipSuccess) p.buf[i] = static_cast<uint32_t *>(q);
+        return GOL_OK;
+    };
+    if (GOL_IPC_SERIAL_OPEN) {
+        int orc = GOL_OK;  // (a rank whose opens failed still takes part in every turn's barrier)
+        for (int turn = 0; turn < nranks && rc == GOL_OK; ++turn) {
+            if (turn == rank) orc = open_peers();
+            rc = c->host_barrier();
         }
-        if (he == hipSuccess) he = hipIpcOpenMemHandle(&q, ps.flags, hipIpcMemLazyEnablePeerAccess);
-        if (he == hipSuccess) p.flags = static_cast<uint32_t *>(q);
-        c->peers_.push_back(p);
-        if (he != hipSuccess) return fail(hip_fail(he, "hipIpcOpenMemHandle"));
+        if (rc == GOL_OK) rc = orc;
+    } else {
+        rc = open_peers();
     }
+    if (rc) return fail(rc);
+    IPC_TRACE("peers opened");
     *out = c;
     return GOL_OK;
 }
