@@ -19,7 +19,8 @@ its halo exchange and the fused AliveCellsCount):
   byte16k  16384 x 16384 byte-per-cell torus, k = 32 turns per launch (config 2); replicas for N > 1.
 
 Inputs are synthetic (splitmix64 Bernoulli(1/2) cells, generated on the GPU) and resident in
-HBM before timing.  Rank 0 prints one JSON line.
+HBM before timing.  Rank 0 prints one JSON line.  (GOL_BENCH_STACKS_AFTER_S=N: every thread's
+Python stack to stderr every N seconds, for a run that seems stuck.)
 """
 from __future__ import annotations
 
