@@ -74,6 +74,7 @@ def rows_sha(words):
     (4, 515, 4096, 0, 41, 1),      # uneven, a count after every turn
     (3, 301, 64 * 40, 8, 22, 11),  # standard layout (W % 1024 != 0), k = 8
     (4, 64, 1024, 0, 30, 10),      # 16-row shards: k capped at 12 by the halo, several launches
+    (8, 1000, 2048, 0, 36, 12),    # N = 8 (config 5's rank count): the ring of 8, uneven rows (125 each)
 ])
 def test_ipc_ranks_match_oracle(G, tmp_path, nranks, H, W, k, turns, every):
     ref, counts = O.bits_run(O.random_words(7, 0, H, W // 64), turns, with_counts=True)
