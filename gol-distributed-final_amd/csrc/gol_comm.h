@@ -30,19 +30,23 @@ struct gol_comm {
 gol_comm *gol_comm_rccl(ncclComm_t c);
 
 // Flag words of an IPC rank (its own device memory, read by its neighbours through IPC):
-// READY = the last exchange whose rows this rank has written (its peers may pull them),
-// PULLED = the last exchange whose ghost rows this rank has copied out of its peers' buffers
-// (its peers may overwrite the rows it read).  Sequence numbers, compared wrap-safe.
-enum { GOL_IPC_READY = 0, GOL_IPC_PULLED = 1, GOL_IPC_FLAG_WORDS = 16 };
+// READY = the last exchange whose send rows this rank has written into its send buffer (its
+// peers may pull them).  A sequence number, compared wrap-safe.  (Until round 5 a PULLED word
+// also ordered board writes behind the peers' pulls; since the peers read only the send buffer,
+// that order is implied by READY, gol_engine.cpp exchange_ipc.)
+enum { GOL_IPC_READY = 0, GOL_IPC_FLAG_WORDS = 16 };
 
 struct gol_ipc_seg;
 
 class gol_ipc final : public gol_comm {
 public:
-    // Join the ranks named by `id` (gol_ipc_unique_id): publish this rank's two bit allocations
-    // (bufs, incl. ghost rows) and flag words, wait until all nranks have joined, map the
-    // buffers of `peers` (global ranks, this one excluded).  Collective.
-    static int open(const uint8_t *id, int nranks, int rank, int device, int64_t H, int64_t W, uint32_t *const bufs[2],
+    // Join the ranks named by `id` (gol_ipc_unique_id): publish this rank's exported allocations
+    // (bufs: the engine passes its halo send buffer; nullptr entries are skipped) and flag words,
+    // wait until all nranks have joined, map the buffers of `peers` (global ranks, this one
+    // excluded).  Collective; every rank must pass the same (nranks, H, W, kx).  A rank whose
+    // join fails marks the segment aborted, so the others fail at their next barrier instead of
+    // waiting out GOL_IPC_TIMEOUT_MS.
+    static int open(const uint8_t *id, int nranks, int rank, int device, int64_t H, int64_t W, int kx, uint32_t *const bufs[2],
                     const std::vector<int> &peers, gol_ipc **out);
     ~gol_ipc() override;
 

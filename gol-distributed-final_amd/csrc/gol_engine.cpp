@@ -324,7 +324,7 @@ extern "C" int gol_engine_create_rank(int64_t H, int64_t W, int32_t nranks, int3
         if (rc == GOL_OK && (hipMemset(s0.ipc_out, 0, ob) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
             rc = gol_set_error(GOL_EHIP, "IPC send rows: hipMemset failed");
         uint32_t *const bufs[2] = {s0.ipc_out, nullptr};
-        if (rc == GOL_OK) rc = gol_ipc::open(id, nranks, rank, dev, H, W, bufs, e->ipc_peers, &e->ipc);
+        if (rc == GOL_OK) rc = gol_ipc::open(id, nranks, rank, dev, H, W, e->kx, bufs, e->ipc_peers, &e->ipc);
         e->comm = e->ipc;
     }
     if (rc != GOL_OK) {
@@ -467,8 +467,8 @@ static int invalidate_halo(gol_engine *e)
             RCCHK(set_dev(s.device));
             HIPCHK(hipStreamWaitEvent(s.stream, s.ev_edge, 0));
             for (auto &t : e->sh) HIPCHK(hipStreamWaitEvent(s.stream, t.ev_halo, 0));  // (loopback: t reads my rows)
-            // IPC: the neighbours have copied my rows of the last exchange out of my buffers
-            if (e->ipc) RCCHK(e->ipc->wait(s.stream, e->ipc_peers, GOL_IPC_PULLED, e->xn, s.err));
+            // (IPC: the neighbours read only this rank's send buffer ipc_out, never its board, and
+            // its own copies into ipc_out are behind ev_halo: nothing to wait for across processes)
         }
     e->halo_ok = false;
     return GOL_OK;
@@ -531,12 +531,12 @@ static bool local_wrap(const gol_engine *e)
 //      into ipc_out slot (xn & 1, op index), then signal READY = xn;
 //   2. wait until each neighbour's READY has reached xn (its send rows for this exchange are in);
 //   3. copy every receive of my gol_halo_plan from the peer's matching send slot (the peer's nth
-//      send to me for my nth receive from it: the pairing RCCL applies to the same plans);
-//   4. signal PULLED = xn.
-// A neighbour overwrites send slot (xn & 1) only at its exchange xn+2, which follows its step
-// after exchange xn+1, which waited for my READY xn+1, which I signal after my step's
-// halo-reading launch, which waited for my pulls of xn: so nothing else orders my copies against
-// its writes.  Writes of the board outside a step wait for PULLED (invalidate_halo).
+//      send to me for my nth receive from it: the pairing RCCL applies to the same plans).
+// A neighbour overwrites send slot (xn & 1) only at its exchange xn+2, which follows (on its comm
+// stream) its exchange xn+1, which waited for my READY xn+1, which I signal on my comm stream
+// after my pulls of xn: so nothing else orders my copies against its writes, whether or not steps
+// run between the exchanges.  Peers never read my board, so writes of the board outside a step
+// (a load, a layout conversion, the exact first turn) need no cross-process wait either.
 static int exchange_ipc(gol_engine *e)
 {
     gol_shard &s = e->sh[0];
@@ -574,7 +574,6 @@ static int exchange_ipc(gol_engine *e)
         HIPCHK(hipMemcpyAsync(s.bits[c] + rv.row * P, out_slot(base, sm), (size_t)rv.rows * P * sizeof(uint32_t),
                               hipMemcpyDeviceToDevice, s.comm));
     }
-    RCCHK(e->ipc->signal(s.comm, GOL_IPC_PULLED, xn));
     HIPCHK(hipEventRecord(s.ev_halo, s.comm));
     e->halo_issued = true;
     return GOL_OK;

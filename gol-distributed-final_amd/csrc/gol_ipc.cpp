@@ -3,7 +3,7 @@
 // The reference's broker ships the whole board to every worker process each turn over TCP
 // (broker.go:143-157, 182-206).  The rank engine keeps each rank's rows resident on its GPU and
 // moves only k halo rows per k turns.  Between the processes of one node this transport moves
-// them without RCCL: every rank exports its two bit buffers and a few flag words with
+// them without RCCL: every rank exports a small halo send buffer and a few flag words with
 // hipIpcGetMemHandle, its ring neighbours map them, and each rank copies its own ghost rows out
 // of its neighbours' HBM (a pull, device to device; the same GPU when ranks share one).  The
 // order between processes is carried by sequence numbers in those flag words, stored and polled
@@ -254,7 +254,7 @@ static bool ipc_trace()
 #define GOL_IPC_SERIAL_OPEN 1
 #endif
 
-int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H, int64_t W, uint32_t *const bufs[2],
+int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H, int64_t W, int kx, uint32_t *const bufs[2],
                   const std::vector<int> &peers, gol_ipc **out)
 {
     *out = nullptr;
@@ -284,14 +284,19 @@ int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H
     c->device_ = device;
     c->timeout_ms_ = ipc_timeout_ms();
     int rc = GOL_OK;
+    gol_ipc_seg *s = c->seg_;
     auto fail = [&](int r) {
+        // the other ranks fail at their next host barrier instead of waiting out the timeout (or,
+        // past the joins, stalling at their first collective or halo wait)
+        s->abort.store(1, std::memory_order_release);
         shm_unlink(name);  // (ENOENT once another rank has removed it)
         delete c;
         return r;
     };
-    gol_ipc_seg *s = c->seg_;
+    // every rank of one board agrees on its shape and on kx (the rows per exchange, which fixes
+    // the halo plans the ranks pair their sends and receives by)
     const uint64_t key = (((uint64_t)nranks * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)H * 0xBF58476D1CE4E5B9ull) ^
-                          ((uint64_t)W * 0x94D049BB133111EBull)) | 1ull;
+                          ((uint64_t)W * 0x94D049BB133111EBull) ^ ((uint64_t)(uint32_t)kx * 0xD6E8FEB86659FD93ull)) | 1ull;
     uint64_t seen = 0;
     if (!s->key.compare_exchange_strong(seen, key) && seen != key)
         return fail(gol_set_error(GOL_EINVAL, "IPC ranks disagree on the board or the rank count"));
@@ -356,6 +361,12 @@ int gol_ipc::open(const uint8_t *id, int nranks, int rank, int device, int64_t H
     } else {
         rc = open_peers();
     }
+    // every rank learns whether any rank's opens failed: a final barrier after which a failed rank
+    // has set abort (fail() below) before any rank returns success
+    if (rc) return fail(rc);
+    rc = c->host_barrier();
+    if (rc == GOL_OK && s->abort.load(std::memory_order_acquire))
+        rc = gol_set_error(GOL_ECOMM, "IPC ranks: another rank failed to join");
     if (rc) return fail(rc);
     IPC_TRACE("peers opened");
     *out = c;

@@ -15,7 +15,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (GOL_IPC_ID_BYTES, GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_WRITE_FN, LAYOUTS, STEP_MODES,
+from ._lib import (GOL_EINVAL, GOL_IPC_ID_BYTES, GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_WRITE_FN, LAYOUTS, STEP_MODES,
                    TRANSPORT_NAMES, TRANSPORTS, GolError, check, gol_config, lib)
 
 
@@ -60,7 +60,13 @@ class Engine:
             self._check(self._L.gol_engine_create(self.H, self.W, ctypes.byref(cfg), ctypes.byref(h)))
         else:
             nranks, rank, uid = _rank
-            idbuf = (ctypes.c_uint8 * len(uid)).from_buffer_copy(uid) if uid is not None else None
+            idbuf = None
+            if uid is not None:
+                # the C side reads exactly GOL_RCCL_ID_BYTES (= GOL_IPC_ID_BYTES) bytes of the id: a
+                # shorter buffer would be read past its end
+                if len(uid) != GOL_RCCL_ID_BYTES or len(uid) != GOL_IPC_ID_BYTES:
+                    raise GolError(GOL_EINVAL, f"rank id must be {GOL_RCCL_ID_BYTES} bytes, got {len(uid)}")
+                idbuf = (ctypes.c_uint8 * GOL_RCCL_ID_BYTES).from_buffer_copy(uid)
             self._check(self._L.gol_engine_create_rank(self.H, self.W, nranks, rank, idbuf, ctypes.byref(cfg),
                                                        ctypes.byref(h)))
         self._h = h

@@ -74,6 +74,16 @@ def test_ipc_unique_id_host_only(G):
     assert G.lib().gol_ipc_unique_id(buf, 16) == G._lib.GOL_EINVAL
 
 
+@pytest.mark.parametrize("n", [0, 24, 127, 129])
+def test_rank_id_of_wrong_length_is_einval(G, n):
+    """Engine.rank checks the id's length before the C call (which reads 128 bytes of it): a short
+    or long id is EINVAL, not an out-of-bounds read."""
+    with pytest.raises(G.GolError) as ei:
+        G.Engine.rank(64, 64, 2, 0, bytes(n), transport="ipc")
+    assert ei.value.code == G._lib.GOL_EINVAL
+    assert "128 bytes" in str(ei.value)
+
+
 @pytest.mark.parametrize("H,T", [(512, 4), (512, 16), (16, 3), (64, 7), (17, 5), (10, 16), (1, 1), (0, 3)])
 def test_partition_matches_broker_formula(G, H, T):
     for i in range(T):

@@ -169,7 +169,7 @@ def test_bench_self_launch_two_replicas():
 
 
 def test_bench_settle_steps_reported():
-    """The clock-settle phase (bench.py --settle-s, default 0.3 s): untimed steps before the
+    """The clock-settle phase (bench.py --settle-s; its default is the parser's): untimed steps before the
     warmup, a fixed count per workload (reproducible turns and counts), reported as
     config.settle_steps and counted in turns_done; the timed steps are exactly --steps launches."""
     import torch
