@@ -189,6 +189,14 @@ class Ranks:
         self.dist.all_reduce(t)
         return float(t.item())
 
+    def gather(self, obj) -> list:
+        """obj of every rank, in rank order (on every rank)."""
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def share(self, obj):
         if self.dist is None:
             return obj
@@ -330,14 +338,17 @@ def run_bits(args, ranks):
                           SETTLE_RATE_BITS)
     if args.warmup:
         e.step_counted(args.warmup * k, k)
+    several = sharded and world > 1
     ranks.barrier()
-    e.set_timing(True)
+    e.set_timing(True, exchanges=several)  # (exchange events only where there are exchanges)
     t0 = time.perf_counter()
     counts = e.step_counted(args.steps * k, k)  # one launch (+ halo exchange + fused count) per step
     dt = time.perf_counter() - t0
     ranks.barrier()
     t = e.timing()
+    x = e.exchange_timing()
     e.set_timing(False)
+    per_rank = rank_stats(ranks, dt, t, x, topo)
     dt = ranks.max(dt)
     alive = int(counts[-1]) if len(counts) else None
     if not sharded and world > 1:
@@ -371,11 +382,34 @@ def run_bits(args, ranks):
            "cells_per_lane": info["cells_per_lane"], "strip_rows": args.strip or "auto",
            "alive_count_every_step": True, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
            "settle_steps": settle, "timed_launches": t["launches"]}
+    if world > 1:
+        cfg["rank_stats"] = per_rank
     if snap:
         cfg["snapshot"] = snap
     e.close()
     dtype = "u32 (bit-packed, 32 cells/word" + (", column-band layout)" if layout == "band" else ")")
     return value, dt, cfg, roof, dtype
+
+
+def rank_stats(ranks, wall_s, timing, xtiming, topo):
+    """What each rank saw of the timed steps, for a run with N > 1 (SCALE's one run must separate
+    compute imbalance from exchange cost): the max / min over ranks of the per-step shard time
+    (HIP events around each stepping call on the compute stream, edge launches and exchange waits
+    included), of the per-exchange time (an event pair around every halo exchange on the stream it
+    runs on: the RCCL send/recv group, or the IPC copies and flag waits), of the wall time, and the
+    rank count each rank's engine reports (RCCL / IPC nranks) with its transport."""
+    mine = {"launch_ms": timing["mean_ms"], "exchange_ms": xtiming["mean_ms"], "exchanges": xtiming["exchanges"],
+            "wall_ms": wall_s * 1e3, "nranks": topo["nranks"], "transport": topo["transport"]}
+    allr = ranks.gather(mine)
+
+    def mm(key):
+        v = [r[key] for r in allr]
+        return {"max": round(max(v), 4), "min": round(min(v), 4)}
+    return {"launch_ms": mm("launch_ms"), "exchange_ms": mm("exchange_ms"), "wall_ms": mm("wall_ms"),
+            "exchanges_per_rank": [r["exchanges"] for r in allr], "nranks_seen": [r["nranks"] for r in allr],
+            "transports": sorted({r["transport"] for r in allr}),
+            "basis": "per rank: launch_ms = mean step time of its shard (HIP events on the compute stream), "
+                     "exchange_ms = mean halo exchange (event pair on the exchange's stream); max / min over ranks"}
 
 
 def settle_steps(args, run_n, cell_updates_per_step, nominal_rate):
@@ -476,8 +510,14 @@ def main():
     ranks = Ranks(args)
     if args.dry_run:
         ranks.barrier()
-        dt = ranks.max(0.001 * (ranks.rank + 1))
+        wall = 0.001 * (ranks.rank + 1)
+        fake_t = {"mean_ms": wall * 1e3 / max(args.steps, 1), "launches": args.steps}
+        fake_x = {"mean_ms": 0.01 * (ranks.rank + 1), "exchanges": args.steps if ranks.world > 1 else 0}
+        per_rank = rank_stats(ranks, wall, fake_t, fake_x, {"nranks": ranks.world, "transport": "dry-run"})
+        dt = ranks.max(wall)
         value, cfg, roof, dtype = 0.0, {"workload": "dry-run", "ranks": ranks.world}, None, None
+        if ranks.world > 1:
+            cfg["rank_stats"] = per_rank
     elif args.workload == "byte16k":
         value, dt, cfg, roof, dtype = run_bytes(args, ranks)
     else:

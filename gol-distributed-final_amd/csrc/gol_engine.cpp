@@ -525,6 +525,9 @@ static bool local_wrap(const gol_engine *e)
     return e->transport == GOL_TRANSPORT_LOCAL && e->sh.size() == 1 && e->nranks == 1;
 }
 
+static int xtime_start(gol_engine *e, gol_shard &s, hipStream_t st, size_t *ev);
+static int xtime_stop(gol_engine *e, gol_shard &s, hipStream_t st, size_t ev, int shard);
+
 // IPC transport (one shard per process): this rank's exchange xn on its comm stream, pulling
 // each ghost block out of the neighbour's send buffer (ipc_out, mapped by the peers):
 //   1. once the rows this rank sends are written (ev_edge), copy every send of my gol_halo_plan
@@ -549,6 +552,8 @@ static int exchange_ipc(gol_engine *e)
     const int64_t slot_words = (int64_t)GOL_GHOST_ROWS * P;
     auto out_slot = [&](uint32_t *base, int m) { return base + ((int64_t)(xn & 1) * 4 + m) * slot_words; };
     HIPCHK(hipStreamWaitEvent(s.comm, s.ev_edge, 0));
+    size_t xev;
+    RCCHK(xtime_start(e, s, s.comm, &xev));
     for (int m = 0; m < 4; ++m)
         if (mine[m].kind == GOL_HALO_SEND) {
             if (mine[m].rows > GOL_GHOST_ROWS) return gol_set_error(GOL_EINVAL, "halo plan: %d rows per send", mine[m].rows);
@@ -574,6 +579,7 @@ static int exchange_ipc(gol_engine *e)
         HIPCHK(hipMemcpyAsync(s.bits[c] + rv.row * P, out_slot(base, sm), (size_t)rv.rows * P * sizeof(uint32_t),
                               hipMemcpyDeviceToDevice, s.comm));
     }
+    RCCHK(xtime_stop(e, s, s.comm, xev, 0));
     HIPCHK(hipEventRecord(s.ev_halo, s.comm));
     e->halo_issued = true;
     return GOL_OK;
@@ -605,6 +611,7 @@ static int exchange(gol_engine *e, bool on_compute = false)
             // are written (theirs)
             for (const auto &op : plans[i])
                 HIPCHK(hipStreamWaitEvent(s.comm, e->sh[local(op.peer)].ev_edge, 0));
+            size_t xev = SIZE_MAX;
             for (int j = 0; j < 4; ++j) {
                 const gol_halo_op &rv = plans[i][j];
                 if (rv.kind != GOL_HALO_RECV) continue;
@@ -618,8 +625,10 @@ static int exchange(gol_engine *e, bool on_compute = false)
                 }
                 if (!sd || sd->rows != rv.rows) return gol_set_error(GOL_EINVAL, "halo plan: unmatched receive");
                 gol_shard &ps = e->sh[p];
+                if (xev == SIZE_MAX) RCCHK(xtime_start(e, s, s.comm, &xev));
                 RCCHK(copy_rows(s, s.bits[c] + rv.row * P, ps, ps.bits[c] + sd->row * P, hb, s.comm));
             }
+            RCCHK(xtime_stop(e, s, s.comm, xev, i));
             HIPCHK(hipEventRecord(s.ev_halo, s.comm));
         }
         e->halo_issued = true;
@@ -636,6 +645,11 @@ static int exchange(gol_engine *e, bool on_compute = false)
             RCCHK(set_dev(s.device));
             HIPCHK(hipStreamWaitEvent(s.comm, s.ev_edge, 0));
         }
+    std::vector<size_t> xev(n);
+    for (int i = 0; i < n; ++i) {
+        RCCHK(set_dev(e->sh[i].device));
+        RCCHK(xtime_start(e, e->sh[i], xs(e->sh[i]), &xev[i]));
+    }
     ncclResult_t first = ncclGroupStart();
     for (int i = 0; i < n && first == ncclSuccess; ++i) {
         gol_shard &s = e->sh[i];
@@ -651,8 +665,10 @@ static int exchange(gol_engine *e, bool on_compute = false)
     const ncclResult_t end = ncclGroupEnd();
     if (first != ncclSuccess || end != ncclSuccess)
         return gol_set_error(GOL_ECOMM, "halo exchange: %s", ncclGetErrorString(first != ncclSuccess ? first : end));
-    for (auto &s : e->sh) {
+    for (int i = 0; i < n; ++i) {
+        gol_shard &s = e->sh[i];
         RCCHK(set_dev(s.device));
+        RCCHK(xtime_stop(e, s, xs(s), xev[i], i));
         HIPCHK(hipEventRecord(s.ev_halo, xs(s)));
     }
     e->halo_issued = true;
@@ -701,6 +717,11 @@ static int fold_timing(gol_engine *e)
         HIPCHK(hipEventSynchronize(s.tev[t.ev + 1]));
         float x = 0;
         HIPCHK(hipEventElapsedTime(&x, s.tev[t.ev], s.tev[t.ev + 1]));
+        if (t.exchange) {
+            e->x_ms += x;
+            e->x_n += 1;
+            continue;
+        }
         e->t_ms += x;
         e->t_cells += t.cell_updates;
         e->t_n += t.steps;
@@ -744,6 +765,26 @@ static int timing_begin(gol_engine *e)
 // A stepping call is being timed (timing_begin .. timing_end): launches outside such a call
 // (gol_engine_step_flips) are not.
 static bool timing_open(const gol_engine *e) { return e->timing && e->tcall_ev.size() == e->sh.size(); }
+
+// GOL_TIMING_EXCHANGE: an event pair around one shard's part of a halo exchange on stream st
+// (xstart before the exchange's first operation on st, xstop after its last).
+static int xtime_start(gol_engine *e, gol_shard &s, hipStream_t st, size_t *ev)
+{
+    *ev = SIZE_MAX;
+    if (!e->timing_x || !timing_open(e)) return GOL_OK;
+    RCCHK(timing_event(e, s, ev));
+    HIPCHK(hipEventRecord(s.tev[*ev], st));
+    return GOL_OK;
+}
+static int xtime_stop(gol_engine *e, gol_shard &s, hipStream_t st, size_t ev, int shard)
+{
+    if (ev == SIZE_MAX) return GOL_OK;
+    HIPCHK(hipEventRecord(s.tev[ev + 1], st));
+    gol_timed t{shard, ev, 0.0, 0};
+    t.exchange = true;
+    e->timed.push_back(t);
+    return GOL_OK;
+}
 
 static int timing_end(gol_engine *e)
 {
@@ -1680,10 +1721,23 @@ extern "C" int gol_engine_set_timing(gol_engine *e, int32_t enable)
         HIPCHK(hipStreamSynchronize(s.stream));
     }
     e->timing = enable != 0;
+    e->timing_x = enable == GOL_TIMING_EXCHANGE;
     e->timed.clear();
     for (auto &s : e->sh) s.tused = 0;
     e->t_ms = e->t_cells = 0;
     e->t_n = 0;
+    e->x_ms = 0;
+    e->x_n = 0;
+    return GOL_OK;
+}
+
+// Local, like gol_engine_timing.
+extern "C" int gol_engine_exchange_timing(gol_engine *e, int64_t *exchanges, double *mean_ms)
+{
+    if (!e || !exchanges || !mean_ms) return gol_set_error(GOL_EINVAL, "bad arguments");
+    RCCHK(fold_timing(e));
+    *exchanges = e->x_n;
+    *mean_ms = e->x_n ? e->x_ms / e->x_n : 0.0;
     return GOL_OK;
 }
 

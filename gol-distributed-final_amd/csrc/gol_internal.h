@@ -79,6 +79,7 @@ struct gol_timed {
     size_t ev;  // index of the start event in the shard's pool (stop = ev + 1)
     double cell_updates;
     int64_t steps;  // k-turn steps between the two events
+    bool exchange = false;  // an event pair around one halo exchange (GOL_TIMING_EXCHANGE), not a stepping call
 };
 
 struct gol_engine {
@@ -114,12 +115,15 @@ struct gol_engine {
     bool halo_on_compute = false;  // the last exchange ran on the compute streams (RCCL after a SERIAL step)
     int64_t pend_first = 0, pend_n = 0;  // count points whose slot arrays await one reduce (flush_counts)
     bool timing = false;
+    bool timing_x = false;             // also an event pair around every halo exchange of a timed call
     std::vector<gol_timed> timed;
     std::vector<size_t> tcall_ev;      // the current stepping call's start events (one per shard)
     std::vector<double> tcall_cells;   // and its cell-updates per shard
     int64_t tcall_steps = 0;           // and its k-turn steps
     double t_ms = 0, t_cells = 0;  // folded timing sums (timed pool recycled)
     int64_t t_n = 0;
+    double x_ms = 0;               // folded exchange timing sums
+    int64_t x_n = 0;
 };
 
 int gol_set_error(int code, const char *fmt, ...);

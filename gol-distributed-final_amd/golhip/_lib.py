@@ -23,6 +23,7 @@ GOL_EQUIT = -7
 GOL_ECOMM = -8
 GOL_COUNT_SLOTS = 256
 GOL_RCCL_ID_BYTES = 128
+GOL_TIMING_EXCHANGE = 2
 GOL_IPC_ID_BYTES = 128
 GOL_IPC_MAX_RANKS = 16
 GOL_LAYOUT_AUTO, GOL_LAYOUT_STANDARD, GOL_LAYOUT_BAND = 0, 1, 2
@@ -125,6 +126,7 @@ SIGNATURES = [
     ("gol_engine_device_bits", ctypes.c_int, [_vp, _P(_vp), _P(_i64)]),
     ("gol_engine_set_timing", ctypes.c_int, [_vp, _i32]),
     ("gol_engine_timing", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double), _P(ctypes.c_double)]),
+    ("gol_engine_exchange_timing", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double)]),
     ("gol_halo_plan", ctypes.c_int, [_i64, _i32, _i32, _i32, _P(gol_halo_op), _i32, _P(_i32)]),
     ("gol_step_plan", ctypes.c_int, [_i64, _i32, _i32, _i32, _P(gol_launch), _i32, _P(_i32)]),
     ("gol_dev_bits_step", ctypes.c_int,

@@ -15,8 +15,8 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (GOL_EINVAL, GOL_IPC_ID_BYTES, GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_WRITE_FN, LAYOUTS, STEP_MODES,
-                   TRANSPORT_NAMES, TRANSPORTS, GolError, check, gol_config, lib)
+from ._lib import (GOL_EINVAL, GOL_IPC_ID_BYTES, GOL_RCCL_ID_BYTES, GOL_SHARDS_SAME_DEVICE, GOL_TIMING_EXCHANGE,
+                   GOL_WRITE_FN, LAYOUTS, STEP_MODES, TRANSPORT_NAMES, TRANSPORTS, GolError, check, gol_config, lib)
 
 
 def rccl_unique_id(library=None) -> bytes:
@@ -223,8 +223,17 @@ class Engine:
         self._check(self._L.gol_engine_shard(self._h, i, ctypes.byref(d), ctypes.byref(a), ctypes.byref(b)))
         return {"device": d.value, "y0": a.value, "y1": b.value}
 
-    def set_timing(self, enable: bool) -> None:
-        self._check(self._L.gol_engine_set_timing(self._h, 1 if enable else 0))
+    def set_timing(self, enable: bool, exchanges: bool = False) -> None:
+        """HIP-event timing of the stepping calls; exchanges=True also times every halo exchange
+        of them (GOL_TIMING_EXCHANGE: one event pair each, on the stream it runs on)."""
+        level = (GOL_TIMING_EXCHANGE if exchanges else 1) if enable else 0
+        self._check(self._L.gol_engine_set_timing(self._h, level))
+
+    def exchange_timing(self) -> dict:
+        """Halo exchanges timed since set_timing(True, exchanges=True) and their mean duration."""
+        n, ms = ctypes.c_int64(), ctypes.c_double()
+        self._check(self._L.gol_engine_exchange_timing(self._h, ctypes.byref(n), ctypes.byref(ms)))
+        return {"exchanges": n.value, "mean_ms": ms.value}
 
     def timing(self) -> dict:
         """HIP-event timing of every shard-step since set_timing(True) (edge launches included)."""

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GOL_ABI_VERSION 4
+#define GOL_ABI_VERSION 5
 
 enum {
     GOL_OK = 0,
@@ -241,6 +241,15 @@ int gol_engine_device_bits(gol_engine *e, uint32_t **bits, int64_t *pitch);
  * (re)enabled, their mean duration and their mean cell-updates (R x W x k). */
 int gol_engine_set_timing(gol_engine *e, int32_t enable);
 int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double *mean_cell_updates);
+/* enable = GOL_TIMING_EXCHANGE (ABI 5): also one event pair around every halo
+ * exchange of a timed stepping call, on the stream the exchange runs on (the
+ * RCCL send/recv group, or the IPC transport's copies and flag waits, from the
+ * moment its sent rows are written); gol_engine_exchange_timing returns how many
+ * were timed since timing was (re)enabled and their mean duration.  Local (this
+ * process's shards); an engine whose one shard is the whole torus exchanges
+ * nothing (0). */
+#define GOL_TIMING_EXCHANGE 2
+int gol_engine_exchange_timing(gol_engine *e, int64_t *exchanges, double *mean_ms);
 
 /* ---------------------------------------------------------------- plans
  * The schedule of a sharded step as data (host functions, no GPU needed).  The

@@ -26,6 +26,15 @@ def test_self_launch_two_ranks_dry_run():
     for key in ("metric", "value", "unit", "steps", "warmup", "higher_is_better", "scaling", "vs_baseline", "dtype",
                 "data", "config", "roofline", "cpu_baseline"):
         assert key in d
+    # N > 1: what each rank saw (bench.rank_stats), so one multi-GPU run separates compute
+    # imbalance (launch_ms spread) from exchange cost (exchange_ms); the dry run's fake per-rank
+    # numbers: rank r steps (r + 1) / steps ms, exchanges 0.01 (r + 1) ms
+    rs = d["config"]["rank_stats"]
+    assert rs["launch_ms"] == {"max": 0.5, "min": 0.25}
+    assert rs["exchange_ms"] == {"max": 0.02, "min": 0.01}
+    assert rs["wall_ms"] == {"max": 2.0, "min": 1.0}
+    assert rs["nranks_seen"] == [2, 2] and rs["exchanges_per_rank"] == [4, 4]
+    assert rs["transports"] == ["dry-run"] and "basis" in rs
 
 
 def test_self_launch_ends_when_a_rank_dies():

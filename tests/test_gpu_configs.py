@@ -120,29 +120,43 @@ def test_config4_rank_shares_tiled(G, H, W):
             _free_engine(e)
 
 
+@pytest.mark.timeout(300)
 def test_config5_bench_workload_exact(G):
-    """The bench's exact workload (bench.py, seed 1, 2^17 x 2^20, 5 + 20 k = 12 launches with the
-    count fused into every launch) as a CROSS-KERNEL check: the 25 counts and the final hash of the
-    band pipeline equal a run of the standard-layout k = 1 kernel (another kernel family, not an
-    independent oracle) counted every 12 turns, and the last count is BENCH_r02's `alive_final`.
-    At this size the oracle itself is too slow; the band pipeline is pinned to the oracle bit for
-    bit by the tiled-torus tests at 65536^2, 262144^2 and 2^20 x 2^20 (below and above)."""
-    H, W = 1 << 17, 1 << 20
+    """The driver's bench command exactly (`bench.py --gpus 1 --steps 20 --warmup 5`: seed 1,
+    2^17 x 2^20, bench.py's own settle steps + 5 warmup + 20 timed k = 12 launches, the count fused
+    into every launch), as a CROSS-KERNEL check: every count and the final hash of the band
+    pipeline equal a run of the standard-layout k = 1 kernel (another kernel family, not an
+    independent oracle) counted every 12 turns, and the last count is the `alive_final` of the
+    driver's line (BENCH_r04.json: 6,080,808,203 at turn 936).  The settle count comes from
+    bench.py itself, so a change of its settle rule or of a kernel that alters the driver's count
+    fails here (count_test.go:44-51 pins counts per turn the same way).  At this size the oracle
+    itself is too slow; the band pipeline is pinned to the oracle bit for bit by the tiled-torus
+    tests at 65536^2, 262144^2 and 2^20 x 2^20 (below and above)."""
+    import bench
+    H, W, k = 1 << 17, 1 << 20, 12
+    args = bench.parse(["--gpus", "1", "--steps", "20", "--warmup", "5"])
+    calls = []
+    settle = bench.settle_steps(args, calls.append, float(H) * W * k, bench.SETTLE_RATE_BITS)
+    launches = settle + args.warmup + args.steps
+    assert calls == [settle] and launches * k == 936, "the driver's turn count changed: re-pin alive_final"
     with G.Engine(H, W, device=0) as e:
-        assert e.info()["turns_per_launch"] == 12 and e.info()["layout"] == "band"
+        assert e.info()["turns_per_launch"] == k and e.info()["layout"] == "band"
         e.load_random(1)
-        band = e.step_counted(5 * 12, 12).tolist() + e.step_counted(20 * 12, 12).tolist()
+        band = []
+        for n in (settle, args.warmup, args.steps):  # bench.run_bits' three stepping calls
+            band += e.step_counted(n * k, k).tolist()
         h_band = e.hash()
         _free_engine(e)
     with G.Engine(H, W, device=0, layout="standard", turns_per_launch=1) as e:
         assert e.info()["turns_per_launch"] == 1
         e.load_random(1)
-        std = e.step_counted(300, 12).tolist()
+        std = e.step_counted(launches * k, k).tolist()
         h_std = e.hash()
         _free_engine(e)
     assert band == std
     assert h_band == h_std
-    assert band[-1] == 8848272907  # BENCH_r02.json config.alive_final (turn 300)
+    assert band[24] == 8848272907  # BENCH_r02.json config.alive_final (turn 300)
+    assert band[-1] == 6080808203  # BENCH_r04.json config.alive_final (turn 936)
 
 
 @pytest.mark.timeout(600)

@@ -202,3 +202,12 @@ def test_bench_share_gpu_shards_over_ipc(G):
     assert two["config"]["alive_final"] == one["config"]["alive_final"]
     k = one["config"]["turns_per_step"]
     assert abs(two["value"] - 4096 * 65536 * k * 3 / (two["ms_per_step"] * 3e-3) / 1e9) < 0.02 * two["value"]
+    # what each rank saw (bench.rank_stats): both ranks' engines report 2 ranks over IPC, every
+    # timed step exchanged its halo once (3 steps), and the per-rank step and exchange times are
+    # live event measurements (the exchange inside the step it precedes is shorter than the step)
+    rs = two["config"]["rank_stats"]
+    assert rs["nranks_seen"] == [2, 2] and rs["transports"] == ["ipc"]
+    assert rs["exchanges_per_rank"] == [3, 3]
+    assert 0 < rs["launch_ms"]["min"] <= rs["launch_ms"]["max"]
+    assert 0 < rs["exchange_ms"]["min"] <= rs["exchange_ms"]["max"] < rs["wall_ms"]["max"]
+    assert "rank_stats" not in one["config"]

@@ -1,4 +1,4 @@
-"""Summarise a tools/profile.sh run into profiles/<tag>/ (tracked):
+"""Summarise a tools/gpu.sh profile run into profiles/<tag>/ (tracked):
   kernel_stats.csv       rocprofv3 --stats summary of the bench command
   pmc_summary.json       per-kernel means of the PMC passes + derived HBM bytes, clock, VALU use
 and update profiles/pmc_traffic.json, read by bench.py for the roofline (HBM bytes and wave64

@@ -6,11 +6,13 @@ registers into the count-slot buffer (which the launch is given instead of count
 one launch of a workload and summarises when workgroups start and end: how much of the kernel
 span the waves are resident, the dispatch ramp, and the tail.
 
-    python tools/timeline.py build [-DFLAG=..]     # here (hipcc), -> tools/tl/libtimeline.so
+    python tools/timeline.py build [-DFLAG=..] [--out NAME]  # here (hipcc), -> tools/variants/libNAME.so
+        # (default libtimeline; the patched sources are built in a temporary directory and removed)
     python tools/timeline.py run bit64k|byte16k|weak|strong2|strong8|strong262k [--strip N] [--wrap] [--pre N]
         # on the GPU box; --wrap: wrap rows read from the board (LOCAL launch), else ghost rows;
         # --pre N: a fill kernel over N x 4096 floats right before the launch
-    python tools/timeline.py build -DGOL_EXP_CLOCK && python tools/timeline.py clock WORKLOAD
+    python tools/timeline.py build -DGOL_EXP_CLOCK --out libclock   # then, on the box:
+    GOL_TL_LIB=tools/variants/libclock.so python tools/timeline.py clock WORKLOAD
         # the shader clock under load: every wave's s_memtime / s_memrealtime (100 MHz) deltas over
         # its life in the last of >= 2 s of back-to-back launches on a random board (median over
         # waves; MI355X_MICROARCH.md 'DVFS give-back' item 6), for dispatches too short for
@@ -24,8 +26,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
-OUT = os.path.join(ROOT, "tools", "tl")
-LIB = os.environ.get("GOL_TL_LIB") or os.path.join(ROOT, "tools", "tl", "libtimeline.so")
+VARIANTS = os.path.join(ROOT, "tools", "variants")
+LIB = os.environ.get("GOL_TL_LIB") or os.path.join(VARIANTS, "libtimeline.so")
 
 ENTRY = "    const int lane = threadIdx.x & 63;\n"
 STAMP_T0 = ENTRY + "    const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();\n    const uint64_t tl_c0 = __builtin_amdgcn_s_memtime(); (void)tl_c0;\n"
@@ -59,8 +61,11 @@ PROF_SPINS = (  # -DGOL_EXP_PROF: cycles each wave spends in its flag waits (rea
 )
 
 
-def build(flags=""):
-    os.makedirs(OUT, exist_ok=True)
+def build(flags="", name="libtimeline"):
+    import shutil
+    import tempfile
+    os.makedirs(VARIANTS, exist_ok=True)
+    OUT = tempfile.mkdtemp(prefix="gol_tl_")
     src = open(os.path.join(CSRC, "gol_kernels.hip")).read()
     if "GOL_EXP_PROF" in flags:
         for stmt, acc in PROF_SPINS:
@@ -83,9 +88,13 @@ def build(flags=""):
         if f.endswith((".cpp", ".h")) or f == "Makefile" or (f.endswith(".hip") and f != "gol_kernels.hip"):
             with open(os.path.join(CSRC, f)) as a, open(os.path.join(OUT, f), "w") as b:
                 b.write(a.read())
-    subprocess.run(["make", "-s", "-j8", "-C", OUT, "ARCH=gfx950", "BUILD=./obj", "OUT=./libtimeline.so",
-                    f"CXXFLAGS=-O3 -std=c++17 -fPIC -Wall -I{ROOT}/include -I. {flags}", f"INC={ROOT}/include"], check=True)
-    print(LIB)
+    lib = os.path.join(VARIANTS, name + ".so")
+    try:
+        subprocess.run(["make", "-s", "-j8", "-C", OUT, "ARCH=gfx950", "BUILD=./obj", f"OUT={lib}",
+                        f"CXXFLAGS=-O3 -std=c++17 -fPIC -Wall -I{ROOT}/include -I. {flags}", f"INC={ROOT}/include"], check=True)
+    finally:
+        shutil.rmtree(OUT, ignore_errors=True)  # (the patched copy of the sources is not kept)
+    print(lib)
 
 
 def run(workload, strip, wrap=False, pre=0):
@@ -255,7 +264,13 @@ if __name__ == "__main__":
         clock(sys.argv[2])
         sys.exit(0)
     if sys.argv[1] == "build":
-        build(" ".join(sys.argv[2:]))  # extra compiler flags, e.g. -DGOL_PIPE_Q=1
+        args = sys.argv[2:]
+        name = "libtimeline"
+        if "--out" in args:
+            i = args.index("--out")
+            name = args[i + 1]
+            del args[i:i + 2]
+        build(" ".join(args), name)  # extra compiler flags, e.g. -DGOL_EXP_CLOCK
     else:
         strip = int(sys.argv[sys.argv.index("--strip") + 1]) if "--strip" in sys.argv else 0
         pre = int(sys.argv[sys.argv.index("--pre") + 1]) if "--pre" in sys.argv else 0
