@@ -641,6 +641,7 @@ __device__ __forceinline__ void lds_wait_n(v4u32 &r)
     else asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(r)::"memory");
 }
 __device__ __forceinline__ void lds_wait1() { asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory"); }
+
 // Wait until `r` (an issued read) has landed, N younger LDS operations left in flight: at a loop
 // back edge, so that the compiler's copies of the loop-carried register read the landed value.
 template <int N>
@@ -696,19 +697,84 @@ __device__ __forceinline__ int spin_until_ge(const lds_u32 *f, int v)
 }
 
 // ------------------------------------------------------------------ band layout, split pipeline
+// Pair step of one stage.  The stage's input stream x_0, x_1, ... arrives in
+// pairs (x_2m, x_2m+1) = (r0, r1); its state holds the horizontal 3-sums of x_2m-2 (a) and
+// x_2m-1 (b) and the cells of x_2m-1 (cb).  It emits the next state of rows 2m-1 and 2m in
+// place of r0, r1 (one row of delay per stage, as a row-by-row stage) and moves its state on by
+// two rows.  The two outputs share the sum of their common rows P = b + c = p0 + 2 p1 + 4 p2
+// (c = x_2m's 3-sums; 4 gates), then each takes a 4-gate tail over (P, the third row's sums, its
+// cell) found by exhaustive search (tools/rule_search_pair.c; tests/test_rule_circuit_cpu.py
+// checks it on every 4 x 3 neighbourhood): with the 2 gates of each row's horizontal sum a
+// generation is 8 ops per 32 cells instead of 9.  The tail relies on the cell's row being one of
+// the pair (the pair sum of a live cell is >= 1, of a dead one <= 5), which holds for both outputs.
+constexpr unsigned TT_PG1 = 0x43;   // (p0, x0, cell)
+constexpr unsigned TT_PG2 = 0x25;   // (p1, p2, x1)
+constexpr unsigned TT_PG3 = 0x8D;   // (p2, cell, g1)
+constexpr unsigned TT_POUT = 0x90;  // (g3, g1, g2)
+__device__ __forceinline__ uint32_t pair_tail(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t x0, uint32_t x1,
+                                              uint32_t cell)
+{
+    const uint32_t g1 = bitop3<TT_PG1>(p0, x0, cell);
+    const uint32_t g2 = bitop3<TT_PG2>(p1, p2, x1);
+    const uint32_t g3 = bitop3<TT_PG3>(p2, cell, g1);
+    return bitop3<TT_POUT>(g3, g1, g2);
+}
+template <int DW>
+struct PairState {
+    uint32_t a0[DW], a1[DW], b0[DW], b1[DW], cb[DW];
+};
+template <int DW>
+__device__ __forceinline__ void pstage(PairState<DW> &s, uint32_t (&r0)[DW], uint32_t (&r1)[DW])
+{
+    // word by word, so that few temporaries are live at once (the pipeline holds 5 KW DW state
+    // registers beside this); a word's 3-sums need its neighbour words' old values, kept until
+    // the words that need them are done.  Order DW-1, 0, 1, .., DW-2: the lane's edge words,
+    // which the next stage's DPP moves read first, come out first (a DPP that reads a VGPR the
+    // previous VALU op wrote waits on an s_nop)
+    const uint32_t l0 = from_lower_lane(r0[DW - 1]), u0 = from_upper_lane(r0[0]);
+    const uint32_t l1 = from_lower_lane(r1[DW - 1]), u1 = from_upper_lane(r1[0]);
+    uint32_t o0[DW], o1[DW];
+#pragma unroll
+    for (int q = 0; q < DW; ++q) {
+#ifdef GOL_PSTAGE_SEQ  // (measurement only: words in order 0 .. DW-1)
+        const int j = q;
+#else
+        const int j = q == 0 ? DW - 1 : q - 1;
+#endif
+        const uint32_t x0 = r0[j], x1 = r1[j];
+        const uint32_t w0 = j == 0 ? l0 : r0[j - 1], w1 = j == 0 ? l1 : r1[j - 1];
+        const uint32_t n0 = j == DW - 1 ? u0 : r0[j + 1], n1 = j == DW - 1 ? u1 : r1[j + 1];
+        const uint32_t c0 = bitop3<TT_XOR3>(w0, x0, n0), c1 = bitop3<TT_MAJ>(w0, x0, n0);
+        const uint32_t d0 = bitop3<TT_XOR3>(w1, x1, n1), d1 = bitop3<TT_MAJ>(w1, x1, n1);
+        const uint32_t k = s.b0[j] & c0;
+        const uint32_t p0 = s.b0[j] ^ c0;
+        const uint32_t p1 = bitop3<TT_XOR3>(s.b1[j], c1, k);
+        const uint32_t p2 = bitop3<TT_MAJ>(s.b1[j], c1, k);
+        o0[j] = pair_tail(p0, p1, p2, s.a0[j], s.a1[j], s.cb[j]);  // row 2m-1: above = x_2m-2
+        o1[j] = pair_tail(p0, p1, p2, d0, d1, x0);                 // row 2m: below = x_2m+1
+        s.a0[j] = c0;
+        s.a1[j] = c1;
+        s.b0[j] = d0;
+        s.b1[j] = d1;
+        s.cb[j] = x1;
+    }
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+        r0[j] = o0[j];
+        r1[j] = o1[j];
+    }
+}
+
 // The K = KW*P stages split over the P waves of one workgroup: wave w runs stages
-// [w*KW, (w+1)*KW) and hands every block of 3 rows to wave w+1 through an LDS ring (3 slots
-// of one block).  A wave then holds 5*KW*4 pipeline VGPRs instead of 5*K*4, which fits 4
-// waves per SIMD.  Wave 0 stages its input rows HBM -> LDS with global_load_lds (no VGPRs),
+// [w*KW, (w+1)*KW) and hands every block of RPB = 2 rows (one pair step) to wave w+1 through an
+// LDS ring of NS = 4 slots.  A wave then holds 5*KW*4 pipeline VGPRs instead of 5*K*4, which fits
+// 4 waves per SIMD.  Wave 0 stages its input rows HBM -> LDS with global_load_lds (no VGPRs),
 // wave P-1 stores to HBM.  Synchronisation is per ring, by LDS flags: ready[e] = blocks
-// published into ring e, consumed[e] = blocks taken out of it; a producer fills slot b % 3
-// once block b-3 is consumed.  Every spin is bounded (spin_until_ge).  1-D grid of work items
+// published into ring e, consumed[e] = blocks taken out of it; a producer fills slot b % NS
+// once block b-NS is consumed.  Every spin is bounded (spin_until_ge).  1-D grid of work items
 // (work_item).
 // COUNT: the last wave adds the alive cells of the rows it stores to a.slots (branch-free: a
-// per-row uniform mask, no branch around the count as a null-slots check made it).
-// ROWF: hand-off flags count rows instead of 3-row blocks, so a reader may read a row as soon as
-// it is written (one-round launches: +1.2 % on 65536^2; the weak board measured -0.4 % and keeps
-// block flags).
+// per-row uniform select, no branch around the count as a null-slots check made it).
 // Role placement (GOL_BAND_PLACE): a workgroup of the band pipeline claims a free slot q (0..3) in
 // its CU's mask and each wave takes pipeline role (its SIMD + q) % 4, so that the (up to) four
 // workgroups resident on a CU put one wave of every role on every SIMD.  (Roles by wave index +
@@ -744,10 +810,13 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
 #ifndef GOL_BAND_LOAD_AUX
 #define GOL_BAND_LOAD_AUX 0
 #endif
-// Pipeline shape of k = 12: KW stages in each of P waves.
+// Pipeline shape of k = 12: KW stages in each of P waves; blocks of GOL_BAND_RPB rows (one pair
+// step), rings of GOL_BAND_NS slots (the role loops are unrolled over the slots).
 #define GOL_BAND_KW 3
 #define GOL_BAND_P 4
-template <int KW, int P, bool CONTIG, bool COUNT, bool ROWF = false>
+#define GOL_BAND_RPB 2
+#define GOL_BAND_NS 4
+template <int KW, int P, bool CONTIG, bool COUNT>
 __global__ void __launch_bounds__(64 * P)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
 band_pipe_kernel(BitsArgs a)
@@ -757,9 +826,11 @@ band_pipe_kernel(BitsArgs a)
     constexpr int HL = band_halo_lanes(K, DW);
     constexpr int U = band_useful_words(K, DW);
     constexpr int ROW = 64 * DW;
-    constexpr int NS = 3;  // (the loops below are unrolled over the 3 slots)
-    __shared__ uint32_t in_ring[NS][3][ROW];
-    __shared__ uint32_t ring_[P - 1][NS][3][ROW];  // ring e+1 in the text = ring[e] here
+    constexpr int RPB = GOL_BAND_RPB;  // rows per block: one pair step
+    constexpr int NS = GOL_BAND_NS;    // (the loops below are unrolled over the NS slots)
+    static_assert(RPB == 2, "a block is one pair step");
+    __shared__ uint32_t in_ring[NS][RPB][ROW];
+    __shared__ uint32_t ring_[P - 1][NS][RPB][ROW];  // ring e+1 in the text = ring[e] here
     __shared__ int ready_[P], consumed_[P];
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (never read; all waves share it)
     __shared__ int place_[P + 2];  // GOL_BAND_PLACE: SIMD of each wave, the CU slot, the mask index
@@ -770,9 +841,7 @@ band_pipe_kernel(BitsArgs a)
     const bool has_rows = work_item(a.sm, a.ngroups, a.row0, a.rows, a.strip, litem, group, s0, s1, rotv);
     uint32_t *ctr;
     const int dir = work_dir(a.sm, litem, ctr);  // 0: static strip, +1 / -1: paired (StripMap)
-    // Pipeline position of this wave, rotated per workgroup: the waves of a workgroup sit on the
-    // CU's SIMDs in wave order, so without the rotation every workgroup on a CU would put its
-    // loader (global_load_lds) on one SIMD and its storer on another.
+    // Pipeline position of this wave, rotated per workgroup (role placement below refines it)
     int wv = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 6) + rotv) % P);
     constexpr bool PLACE = GOL_BAND_PLACE && P == 4;
 
@@ -786,11 +855,14 @@ band_pipe_kernel(BitsArgs a)
     const int R = (int)a.R;
     const int first_in = s0 - K;
     const int last_in = s1 + K - 1;
-    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
-    // a pair's range, stretched to s1e so that 9 (3 blocks of 3 rows: one loop trip) divide its
-    // len + 4K; rows past s1 are read clamped and never stored
-    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + 8) / 9) * 9 - 4 * K : s1;
-    const int nclaim = (s1e - s0 + 4 * K) / 3;  // blocks of the pair (a multiple of 3)
+    // the stream: input row first_in + t at stream step t (walking up, dir -1: s1e + K - 1 - t);
+    // output row first_in + t - K (s1e - 1 + 2K - t), valid from step 2K on
+    const int nblk = ((s1 - s0) + 2 * K + RPB - 1) / RPB;
+    constexpr int TRIP = RPB * NS;  // rows per loop trip
+    // a pair's range, stretched to s1e so that TRIP divides its len + 4K (whole loop trips); rows
+    // past s1 are read clamped and never stored
+    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + TRIP - 1) / TRIP) * TRIP - 4 * K : s1;
+    const int nclaim = (s1e - s0 + 4 * K) / RPB;  // blocks of the pair (a multiple of NS)
 
     const int pitch_b = (int)a.pitch * 4;
     const char *mid_b = reinterpret_cast<const char *>(a.mid);
@@ -802,12 +874,10 @@ band_pipe_kernel(BitsArgs a)
 
     // wave 0: block b -> in_ring[b % NS] (global_load_lds).  The slot is an argument: a lambda
     // that captures a __shared__ array silently loses the kernel's host-side stub.
-    // (one row address per row: the byte pipeline's interior-block stepping measured −4 % here on
-    // 65536², equal on the weak board: the band loader is not bound by its scalar instructions)
     auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            const int t = 3 * b + s;  // stream position
+        for (int s = 0; s < RPB; ++s) {
+            const int t = RPB * b + s;  // stream position
             int y = dir >= 0 ? first_in + t : s1e + K - 1 - t;
             y = y > last_in ? last_in : (y < first_in ? first_in : y);
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
@@ -836,28 +906,33 @@ band_pipe_kernel(BitsArgs a)
     lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready_[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed_[0];
-    constexpr int SLOT = 3 * ROW;  // uint32 per slot (one block)
+    constexpr int SLOT = RPB * ROW;  // uint32 per slot (one block)
 
-    Pipe<KW, DW> p;
-    pipe_init(p);
+    PairState<DW> st[KW];
+#pragma unroll
+    for (int g = 0; g < KW; ++g)
+#pragma unroll
+        for (int j = 0; j < DW; ++j) { st[g].a0[j] = 0; st[g].a1[j] = 0; st[g].b0[j] = 0; st[g].b1[j] = 0; st[g].cb[j] = 0; }
     uint32_t alive = 0;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
     int seen_ready = 0, seen_free = 0;  // cached flag values (ring wv ready, ring wv+1 consumed)
     const uint32_t nrows = (uint32_t)(s1 - s0);
-    // One loop per role (0 = loader, 1 = middle, 2 = last), unrolled over the 3 ring slots so
+    // One loop per role (0 = loader, 1 = middle, 2 = last), unrolled over the NS ring slots so
     // every LDS address is a per-lane register plus an immediate offset and every wait count is
-    // a constant.  The loop carries no other per-block arithmetic than the flag values: the
-    // per-block instruction count is what bounds this kernel (all waves issue through the same
-    // per-SIMD slots, so scalar and branch instructions cost about as much as VALU ones).
-    //  * row S+1 is read while row S computes; a row wait leaves the youngest LDS operation
-    //    (this wave's previous ds_write or flag write) in flight: lgkmcnt(1);
-    //  * the reading waves issue row 0 of block b+1 at row 2 of block b (spinning there if its
-    //    flag is not yet seen), then write "block b consumed";
-    //  * a writing wave publishes "blocks < b ready" after computing row 0 of block b, when its
-    //    writes of block b-1 are done (lgkmcnt(1) leaves only the row-1 read in flight);
-    //  * the block count is padded to a multiple of 3: padding blocks read clamped rows and
+    // a constant.  Per block b (LDS operations of a wave complete in order):
+    //  * wait for block b's two rows (read at the end of block b-1, the wave's youngest LDS
+    //    operations: lgkmcnt(0), which also completes block b-1's row writes);
+    //  * readers: write "block b consumed"; writers: publish "blocks < b ready";
+    //  * compute the pair through the wave's KW stages;
+    //  * writers: make sure slot b % NS is free, write the two rows; the last wave stores them
+    //    to HBM;
+    //  * readers: make sure block b+1 is published; the loader instead refills block b-2's slot
+    //    with block b+2 (global_load_lds) and waits (vmcnt) for block b+1's; read block b+1's rows;
+    //  * the block count is padded to a multiple of NS: padding blocks read clamped rows and
     //    their stores fall outside the strip's buffer range.
-    const int nblk3 = (nblk + 2) / 3 * 3;
+    //  (Reading the next rows before the compute instead holds 8 more VGPRs across it: the kernel
+    //  then spills at 128.)
+    const int nblkT = (nblk + NS - 1) / NS * NS;
     constexpr int SB = SLOT * 4, RB = ROW * 4;  // slot and row strides in bytes
     lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
     lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // writer: ring wv+1 ready
@@ -865,58 +940,45 @@ band_pipe_kernel(BitsArgs a)
     lds_u32 *const in_base = in_l + lane * 4;
     lds_u32 *const rd_base = ring_l + (wv - 1) * NS * SLOT + lane * 4;  // ring wv (wv >= 1)
     lds_u32 *const wr_base = ring_l + wv * NS * SLOT + lane * 4;        // ring wv+1 (wv < P-1)
-    auto compute = [&](auto s_c, uint32_t (&cur)[DW]) {
-        constexpr int S = decltype(s_c)::value;
-#pragma unroll
-        for (int g = 0; g < KW; ++g) bstage_seq<KW, DW, S>(p, g, cur);
-    };
     auto unpack = [&](const v4u32 v, uint32_t (&cur)[DW]) { cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w; };
     auto pack = [&](const uint32_t (&cur)[DW]) { return v4u32{cur[0], cur[1], cur[2], cur[3]}; };
-    // writer, after row 0 of block b: publish blocks < b, then make sure slot b % 3 is free
-    auto publish_and_reserve = [&](int b) -> bool {
-        lds_wait1();
-        lds_flag_wr(rdy_addr, ROWF ? 3 * b : b);
-        if (seen_free < b + 1 - NS) {
-            seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
-            if (seen_free < 0) return false;
-        }
-        return true;
-    };
-    // last wave: output row y = s0 + 3b + S - 2K, stored at voffset lane_off + (y - s0) * pitch
+    // last wave: output row y = s0 + 2b + S - 2K, stored at voffset lane_off + (y - s0) * pitch
     // of a buffer spanning the strip's rows: rows before s0 (negative offsets, as unsigned
     // >= 2^32 - 2K * pitch) and from s1 on fall outside it, and so does a halo lane's 2^31.
     const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
         dst_b + (int64_t)s0 * pitch_b, (short)0, (int)(nrows * (uint32_t)pitch_b), 0x00020000);
-    // (walking up, dir -1: output row y = s1e - 1 + 2K - 3b - S, offsets decreasing)
+    // (walking up, dir -1: output row y = s1e - 1 + 2K - 2b - S, offsets decreasing)
     int rrel = dir >= 0 ? -2 * K : s1e - 1 + 2 * K - s0;  // output row - s0 (wave-uniform)
     const int rstep = dir >= 0 ? 1 : -1;
     uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch_b;
     const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch_b;
     auto emit = [&](const uint32_t (&cur)[DW]) {
         __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, GOL_BAND_STORE_AUX);
-        // fused count of the rows this strip stores (v_bcnt accumulates; halo lanes are masked
-        // once at the end)
+        // fused count of the rows this strip stores: a v_bcnt chain that accumulates, kept only
+        // for the strip's rows (a uniform select; halo lanes are masked once at the end)
+        // (written as a chain, compiled to v_bcnt pairs + v_add3 + a select: forcing the chain with
+        // inline asm costs an s_nop after each asm statement, the hazard recognizer cannot see in)
         if constexpr (COUNT) {
-            const uint32_t m = (uint32_t)rrel < nrows ? 0xFFFFFFFFu : 0u;
-            alive += (__popc(cur[0]) + __popc(cur[1]) + __popc(cur[2]) + __popc(cur[3])) & m;
+            const uint32_t c = __popc(cur[3]) + (__popc(cur[2]) + (__popc(cur[1]) + (__popc(cur[0]) + alive)));
+            alive = (uint32_t)rrel < nrows ? c : alive;
         }
         voff += vstep;
         rrel += rstep;
     };
     lds_u32 *const src_base = wv == 0 ? in_base : rd_base;
-    // paired: the loader's claims, 3 blocks (one loop trip) each, one in flight (issued at row 2
-    // of a trip's first block, used at the next trip's start); the first before block 0's loads
+    // paired: the loader's claims, NS blocks (one loop trip) each, one in flight (issued at a
+    // trip's first block, used at the next trip's start); the first before block 0's loads
     constexpr int FINAL = 1 << 30;  // ready flag = FINAL + blocks: the stream has ended
     // (lane 0 claims; the kernels are built without the atomic optimizer, which broadcast the
     // claim's return at once and so waited for it right there: an atomic round trip per trip)
     uint32_t pending = 0;
-    if (wv == 0 && dir && lane == 0) pending = atomicAdd(ctr, 3u);
-    // block 0's row 0, read to completion here (the compiler copies the loop-carried register
+    if (wv == 0 && dir && lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
+    // block 0's rows, read to completion here (the compiler copies the loop-carried registers
     // on loop entry, which must not happen while a read is in flight)
     if (wv == 0) {
         stage_in(0, in_ring[0]);
         stage_in(1, in_ring[1]);
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     } else if (seen_ready < 1) {
         seen_ready = spin_until_ge(ready_l + wv, 1);
         if (seen_ready < 0) {
@@ -924,8 +986,10 @@ band_pipe_kernel(BitsArgs a)
             return;
         }
     }
-    v4u32 nextv = lds_rd128(src_base);
-    lds_flag_wr(wv == 0 ? scratch : cns_addr, 0);  // one younger LDS operation for block 0's wait
+    v4u32 nx0 = lds_rd128_issue_o<0>(src_base);
+    v4u32 nx1 = lds_rd128_issue_o<RB>(src_base);
+    lds_wait_n<0>(nx0);
+    lds_wait_n<0>(nx1);
     // readers: the block the loop is about to run exists (an empty paired stream ends at once)
     bool more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
     auto step = [&](int b, auto u_c, auto role_c, auto dyn_c, auto skip_c) -> bool {
@@ -934,121 +998,105 @@ band_pipe_kernel(BitsArgs a)
         constexpr bool DYN = decltype(dyn_c)::value;
         constexpr bool SKIP = decltype(skip_c)::value;  // a fill block: no rule (see run)
         constexpr bool LAST = ROLE == 2;
-        uint32_t cur[DW];
-        auto realign = [&]() {
-            if (ROLE == 0 && wrap) {
-#pragma unroll
-                for (int j = 0; j < DW; ++j) cur[j] = __builtin_amdgcn_alignbit(cur[j], cur[j], rot);
-            }
-        };
-        // row 0
-        lds_wait_n<1>(nextv);  // younger: the consumed flag / scratch write, the previous row-2 write
-        unpack(nextv, cur);
-        if (ROWF && ROLE != 0 && seen_ready < 3 * b + 2) {  // row 3b + 1 written
-            seen_ready = spin_until_ge(ready_l + wv, 3 * b + 2);
-            if (seen_ready < 0) return false;
-        }
-        nextv = lds_rd128_issue_o<US * SB + RB>(src_base);
-        realign();
-        if constexpr (!SKIP) compute(std::integral_constant<int, 0>(), cur);
-        if constexpr (LAST) {
-            emit(cur);
-        } else {
-            if (!publish_and_reserve(b)) return false;
-            lds_wr128_o<US * SB>(wr_base, pack(cur));
-        }
-        // row 1
-        lds_wait_n<LAST ? 0 : 1>(nextv);
-        unpack(nextv, cur);
-        if (ROWF && ROLE != 0 && seen_ready < 3 * b + 3) {  // row 3b + 2 written
-            seen_ready = spin_until_ge(ready_l + wv, 3 * b + 3);
-            if (seen_ready < 0) return false;
-        }
-        nextv = lds_rd128_issue_o<US * SB + 2 * RB>(src_base);
-        realign();
-        if constexpr (!SKIP) compute(std::integral_constant<int, 1>(), cur);
-        if constexpr (LAST) emit(cur);
-        else {
-            if constexpr (ROWF) {  // rows < 3b + 1 written (row 3b's write is older than the row-2 read)
-                lds_wait1();
-                lds_flag_wr(rdy_addr, 3 * b + 1);
-            }
-            lds_wr128_o<US * SB + RB>(wr_base, pack(cur));
-        }
-        // row 2; row 0 of block b+1 is read during it
-        lds_wait_n<LAST ? 0 : 1>(nextv);
-        unpack(nextv, cur);
+        constexpr int NXT = (US + 1) % NS;
+        uint32_t r0[DW], r1[DW];
+        // block b's rows, the youngest LDS operations of this wave: once they are in, so are
+        // block b-1's row writes, and both flags can go out at once
+        lds_settle<0>(nx0);
+        lds_settle<0>(nx1);
+        unpack(nx0, r0);
+        unpack(nx1, r1);
+        if constexpr (ROLE != 0) lds_flag_wr(cns_addr, b + 1);  // block b's slot is free
+        if constexpr (!LAST) lds_flag_wr(rdy_addr, b);          // blocks < b are in ring wv+1
         if constexpr (ROLE == 0) {
-            stage_in(b + 2, in_ring[(US + 2) % 3]);  // refills block b-1's slot (clamped past the end)
-            // block b+1 landed, b+2 in flight (and, paired, at US 1 the claim issued at US 0)
-            if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            if constexpr (DYN && US == 0) {
-                if (lane == 0) pending = atomicAdd(ctr, 3u);
+            if (wrap) {
+#pragma unroll
+                for (int j = 0; j < DW; ++j) {
+                    r0[j] = __builtin_amdgcn_alignbit(r0[j], r0[j], rot);
+                    r1[j] = __builtin_amdgcn_alignbit(r1[j], r1[j], rot);
+                }
             }
-            nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
-            lds_flag_wr(scratch, 0);
+        }
+        if constexpr (!SKIP) {
+#pragma unroll
+            for (int g = 0; g < KW; ++g) pstage<DW>(st[g], r0, r1);
+        }
+        if constexpr (LAST) {
+            emit(r0);
+            emit(r1);
+        } else {
+            if (seen_free < b + 1 - NS) {  // slot b % NS: block b - NS consumed
+                seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
+                if (seen_free < 0) return false;
+            }
+            lds_wr128_o<US * SB>(wr_base, pack(r0));
+            lds_wr128_o<US * SB + RB>(wr_base, pack(r1));
+        }
+        // block b+1's rows: read now, waited for at the next block's start (the compute of the
+        // other waves of the SIMD covers the LDS latency)
+        if constexpr (ROLE == 0) {
+            stage_in(b + 2, in_ring[(US + 2) % NS]);  // refills block b-2's slot (clamped past the end)
+            // block b+1 landed, b+2 in flight (and, paired, at US 1 the claim issued at US 0)
+            if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            if constexpr (DYN && US == 0) {
+                if (lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
+            }
         } else {
             // the next block exists unless the writer's flag says the stream ended before it
-            const int need = ROWF ? 3 * b + 4 : b + 2;  // (row 0 of) block b+1 written
-            if (seen_ready < need) {
-                seen_ready = spin_until_ge(ready_l + wv, need);
+            if (seen_ready < b + 2) {
+                seen_ready = spin_until_ge(ready_l + wv, b + 2);
                 if (seen_ready < 0) return false;
             }
-            more = seen_ready < FINAL || (ROWF ? 3 * (b + 1) : b + 1) < seen_ready - FINAL;
-            if (more) nextv = lds_rd128_issue_o<((US + 1) % 3) * SB>(src_base);
-            lds_flag_wr(cns_addr, b + 1);
+            more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
         }
-        realign();
-        if constexpr (!SKIP) compute(std::integral_constant<int, 2>(), cur);
-        if constexpr (LAST) emit(cur);
-        else {
-            if constexpr (ROWF) {  // rows < 3b + 2 written
-                lds_wait1();
-                lds_flag_wr(rdy_addr, 3 * b + 2);
-            }
-            lds_wr128_o<US * SB + 2 * RB>(wr_base, pack(cur));
-        }
+        nx0 = lds_rd128_issue_o<NXT * SB>(src_base);  // (past the stream's end: a stale slot, unused)
+        nx1 = lds_rd128_issue_o<NXT * SB + RB>(src_base);
         return true;
     };
-    // blocks the loader has: nblk3, or (paired) the claims granted so far
-    auto grant = [&](uint32_t c) { return c >= (uint32_t)nclaim ? 0 : 3; };
+    // blocks the loader has: nblkT, or (paired) the claims granted so far
+    auto grant = [&](uint32_t c) { return c >= (uint32_t)nclaim ? 0 : NS; };
+    auto trip = [&](int b, auto role_c, auto dyn_c, auto skip_c) -> bool {
+        return step(b, std::integral_constant<int, 0>(), role_c, dyn_c, skip_c) &&
+               step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c, skip_c) &&
+               step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c, skip_c) &&
+               step(b + 3, std::integral_constant<int, 3>(), role_c, dyn_c, skip_c);
+    };
+    static_assert(NS == 4, "trip() runs NS steps");
     auto run = [&](auto role_c, auto dyn_c) -> bool {
         constexpr int ROLE = decltype(role_c)::value;
         constexpr bool DYN = decltype(dyn_c)::value;
-        int nb = DYN ? 0 : nblk3;
+        int nb = DYN ? 0 : nblkT;
         int b = 0;
-        // Fill blocks: stage g's input is valid from stream step 2g on, and its state of the
-        // steps before 2g only feeds outputs of steps before 2g + 2, which no later stage uses
-        // (the last stage's rows before step 2K fall outside the strip).  A wave whose first
-        // stage is g0 = KW * wv therefore passes the blocks that end before step 2 g0
-        // (3b + 2 < 2 g0) on without the rule -- whole loop trips of them, in a loop of their
-        // own (a branch per block inside the main loop made the compiler spill).  Launches of
-        // many rounds only: same box, weak +0.5 %, 262144² +0.7 %, but the one-round ROWF
-        // launch (65536²) -2 % (profiles/r03/r03r_ab_fill.jsonl).
-        if constexpr (ROLE != 0 && !ROWF) {
-            const int nskip = (2 * KW * wv) / 3;
-            for (; b + 3 <= nskip; b += 3) {
+        // Fill blocks: stage g's input is valid from stream step 2g on, and a stage whose state
+        // missed the steps before S emits garbage only up to step S + 1, which no later stage uses
+        // if S <= 2g (stage g's outputs are read from step 2g + 2 on; the last stage's rows before
+        // step 2K fall outside the strip).  A wave whose first stage is g0 = KW * wv therefore
+        // passes the blocks before step 2 g0 (2b + 1 < 2 g0: b < g0) on without the rule -- whole
+        // loop trips of them, in a loop of their own (a branch per block inside the main loop made
+        // the compiler spill).
+        if constexpr (ROLE != 0) {
+            const int nskip = KW * wv;
+            for (; b + NS <= nskip; b += NS) {
                 if (!more) break;
-                if (!step(b, std::integral_constant<int, 0>(), role_c, dyn_c, std::true_type())) return false;
-                if (!step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c, std::true_type())) return false;
-                if (!step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c, std::true_type())) return false;
+                if (!trip(b, role_c, dyn_c, std::true_type())) return false;
             }
         }
-        for (;; b += 3) {
+        for (;; b += NS) {
             if constexpr (ROLE == 0) {
                 if constexpr (DYN) nb += grant(__builtin_amdgcn_readfirstlane(pending));
                 if (b >= nb) break;
             } else {
                 if (!more) break;
             }
-            if (!step(b, std::integral_constant<int, 0>(), role_c, dyn_c, std::false_type())) return false;
-            if (!step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c, std::false_type())) return false;
-            if (!step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c, std::false_type())) return false;
+            if (!trip(b, role_c, dyn_c, std::false_type())) return false;
         }
+        // the last block's reads of the next slot are still in flight: land them before their
+        // registers are used for anything else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (ROLE != 2) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_flag_wr(rdy_addr, FINAL + (ROWF ? 3 * b : b));
+            lds_flag_wr(rdy_addr, FINAL + b);
         }
         if constexpr (ROLE == 0 && DYN) {
             if (lane == 0 && atomicAdd(ctr + 1, 1u) == 1u) {  // both loaders' claims are over
@@ -1084,33 +1132,20 @@ band_pipe_kernel(BitsArgs a)
 // 65536^2 139.8 vs 137.2) and the byte pipeline 4.5 % slower (56.8 vs 59.4);
 // profiles/r04/r04h_sched.jsonl.
 using namespace golk;
-const void *golk_band_pipe_fn(bool contig, bool count, bool rowf)
+const void *golk_band_pipe_fn(bool contig, bool count)
 {
     constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
-    if (rowf)
-        return contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true, true> : (const void *)band_pipe_kernel<KW, P, true, false, true>)
-                      : (count ? (const void *)band_pipe_kernel<KW, P, false, true, true> : (const void *)band_pipe_kernel<KW, P, false, false, true>);
     return contig ? (count ? (const void *)band_pipe_kernel<KW, P, true, true> : (const void *)band_pipe_kernel<KW, P, true, false>)
                   : (count ? (const void *)band_pipe_kernel<KW, P, false, true> : (const void *)band_pipe_kernel<KW, P, false, false>);
 }
-hipError_t golk_band_pipe_launch(bool contig, bool count, bool rowf, unsigned nwg, const BitsArgs &a, hipStream_t s)
+hipError_t golk_band_pipe_launch(bool contig, bool count, unsigned nwg, const BitsArgs &a, hipStream_t s)
 {
     constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
     const dim3 g(nwg), blk(64 * P);
-    if (rowf) {
-        if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true, true>), g, blk, 0, s, a);
-        else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false, true>), g, blk, 0, s, a);
-        else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true, true>), g, blk, 0, s, a);
-        else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false, true>), g, blk, 0, s, a);
-    } else if (contig && count) {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), g, blk, 0, s, a);
-    } else if (contig) {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false>), g, blk, 0, s, a);
-    } else if (count) {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), g, blk, 0, s, a);
-    } else {
-        hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false>), g, blk, 0, s, a);
-    }
+    if (contig && count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, true>), g, blk, 0, s, a);
+    else if (contig) hipLaunchKernelGGL((band_pipe_kernel<KW, P, true, false>), g, blk, 0, s, a);
+    else if (count) hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, true>), g, blk, 0, s, a);
+    else hipLaunchKernelGGL((band_pipe_kernel<KW, P, false, false>), g, blk, 0, s, a);
     return hipGetLastError();
 }
 #else  // the rest of the kernels and the host side
@@ -1307,93 +1342,59 @@ __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
 
 // Byte board, split pipeline: K = KW * P turns per launch, P waves per workgroup on one
 // column group of 62 words (32 cells per lane, standard bit layout in registers, shifted
-// frame), KW stages per wave, 3-row blocks handed on through LDS rings (256 B per row) with
-// the flag protocol of band_pipe_kernel.  Wave 0 loads and packs the bytes, wave P-1
-// realigns, unpacks and stores them.  One 32-cell word per lane covers K <= 32 columns of
-// halo, so K = 32 costs no more lanes than K = 16, and the 16384^2 board gets P waves per
-// column group instead of one (the one-wave kernel runs at ~1 wave per SIMD there).
-// Rows S = 0, 1, 2 of one ring slot (ROW = 64 uint32 apart), read and waited for together.
-__device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
+// frame), KW stages per wave, blocks of 2 rows (one pair step, as band_pipe_kernel) handed on
+// through LDS rings of NS slots (256 B per row) with band_pipe_kernel's flag protocol and loop
+// shape: one loop per role, unrolled over the NS slots (every LDS address a register plus an
+// immediate, no slot arithmetic, no per-block branch for the fill blocks).  Wave 0 stages its
+// input blocks HBM -> LDS with global_load_lds and packs 32 bytes per lane into one word with
+// v_dot4_i32_i8; wave P-1 realigns (after 32 stages the frame shift is exactly one word),
+// unpacks through a 2 KiB LDS table (byte -> 8 bytes of 0x00 / 0xFF) and stores the strip
+// through one buffer descriptor with a running offset.  One 32-cell word per lane covers K <= 32
+// columns of halo, so K = 32 costs no more lanes than K = 16.
+// (Round 4's form -- 3-row blocks, one block per loop trip with running slot indices and a
+// per-block fill branch -- spent 0.44 scalar instructions per VALU: DESIGN.md §4.4.)
+//
+// Shifted-frame pair step: pstage's circuit on this frame.  A row's 3-sum at bit p is
+// c[p] + c[p-1] + c[p-2] (centred on p-1: the neighbour from the lower lane by one DPP, two
+// v_alignbit), the cell is c[p-1]; every stage moves the frame one bit to the left.
+__device__ __forceinline__ void spstage(PairState<1> &s, uint32_t &r0, uint32_t &r1)
 {
-    asm volatile(
-        "ds_read_b32 %0, %3\n\t"
-        "ds_read_b32 %1, %3 offset:256\n\t"
-        "ds_read_b32 %2, %3 offset:512\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
-        : "v"(p)
-        : "memory");
-}
-
-// The same three reads without the wait, and the wait (the values are in-out operands, so no
-// use of them moves above it).
-__device__ __forceinline__ void lds_rd32x3_issue(const lds_u32 *p, uint32_t (&r)[3])
-{
-    asm volatile(
-        "ds_read_b32 %0, %3\n\t"
-        "ds_read_b32 %1, %3 offset:256\n\t"
-        "ds_read_b32 %2, %3 offset:512"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
-        : "v"(p)
-        : "memory");
-}
-__device__ __forceinline__ void lds_wait3(uint32_t (&r)[3])
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2])::"memory");
+    const uint32_t w0 = from_lower_lane(r0), w1 = from_lower_lane(r1);
+    const uint32_t l0 = __builtin_amdgcn_alignbit(r0, w0, 31), m0 = __builtin_amdgcn_alignbit(r0, w0, 30);
+    const uint32_t l1 = __builtin_amdgcn_alignbit(r1, w1, 31), m1 = __builtin_amdgcn_alignbit(r1, w1, 30);
+    const uint32_t c0 = bitop3<TT_XOR3>(l0, r0, m0), c1 = bitop3<TT_MAJ>(l0, r0, m0);
+    const uint32_t d0 = bitop3<TT_XOR3>(l1, r1, m1), d1 = bitop3<TT_MAJ>(l1, r1, m1);
+    const uint32_t k = s.b0[0] & c0;
+    const uint32_t p0 = s.b0[0] ^ c0;
+    const uint32_t p1 = bitop3<TT_XOR3>(s.b1[0], c1, k);
+    const uint32_t p2 = bitop3<TT_MAJ>(s.b1[0], c1, k);
+    r0 = pair_tail(p0, p1, p2, s.a0[0], s.a1[0], s.cb[0]);  // row 2m-1: its cell = c[p-1] of x_2m-1
+    r1 = pair_tail(p0, p1, p2, d0, d1, l0);                 // row 2m: its cell = c[p-1] of x_2m
+    s.a0[0] = c0;
+    s.a1[0] = c1;
+    s.b0[0] = d0;
+    s.b1[0] = d1;
+    s.cb[0] = l1;
 }
 
 #ifndef GOL_BYTES_PER_CU
 #define GOL_BYTES_PER_CU 3  // workgroups per CU of a one-round launch
 #endif
-// Ring slots per inter-wave ring of the byte pipeline: 4 measured +1.5 % over 3 (16384^2, same
-// box), 6 (with NSI = 3 below, which alone cost 0.6 %, and one flag-scratch row for all waves:
-// 53 KiB per workgroup, still 3 per CU) +1.3-3 % over 4; role order reversed on each SIMD (the
-// older wave of a SIMD the downstream one) -5 %; with the hand-off software-pipelined (reads one block ahead, no wait for own writes)
-// the byte pipeline ran within 2 % of the blocking version, and 4 x 8-stage waves equal to 8 x 4:
-// at ~0.45-0.49 of the VALU issue roof neither the hand-off nor the HBM streams (no loads and
-// no stores: +10 %) bound it.
+// Ring slots of the byte pipeline (input and hand-off rings; the role loops are unrolled over them)
 #ifndef GOL_BYTES_NS
-#define GOL_BYTES_NS 6
+#define GOL_BYTES_NS 4
 #endif
-// Input ring of the byte pipeline's first wave: blocks of 3 byte rows staged HBM -> LDS with
-// global_load_lds (no VGPRs), NSI - 1 blocks in flight while the wave packs and computes one.
-#ifndef GOL_BYTES_NSI
-#define GOL_BYTES_NSI 3
-#endif
-// The six 16-byte halves of one input block (row S: lo at S * 2 KiB, hi at S * 2 KiB + 1 KiB,
-// lane * 16 within each), read and waited for together.
-__device__ __forceinline__ void lds_rd_block6(const lds_u32 *p, v4u32 (&r)[6])
+template <int KW, int P, bool COUNT>
+__global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 8))) bytes_pipe_kernel(BytesKArgs a)
 {
-    asm volatile(
-        "ds_read_b128 %0, %6\n\t"
-        "ds_read_b128 %1, %6 offset:1024\n\t"
-        "ds_read_b128 %2, %6 offset:2048\n\t"
-        "ds_read_b128 %3, %6 offset:3072\n\t"
-        "ds_read_b128 %4, %6 offset:4096\n\t"
-        "ds_read_b128 %5, %6 offset:5120\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5])
-        : "v"(p)
-        : "memory");
-}
-// 1-D grid of work items (work_item).  P waves of one column group: wave 0 loads its input
-// byte rows (one 3-row block ahead, in registers) and packs them with v_dot4_i32_i8, runs KF
-// stages and hands the block on; waves 1 .. P-2 run KM stages each; wave P-1 runs KL stages,
-// realigns the frame, unpacks through a 2 KiB LDS table (byte value -> 8 bytes of 0x00 / 0xFF)
-// and stores.  The first and last waves carry the byte conversion, so they get fewer stages
-// (a wave that is busy when its consumer wants the next block sets the pipeline's rate).
-// One loop per role (no role branches inside the loop).
-template <int KF, int KM, int KL, int P, bool COUNT>
-__global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
-{
-    constexpr int K = KF + (P - 2) * KM + KL;
-    constexpr int KX = KM > KF ? (KM > KL ? KM : KL) : (KF > KL ? KF : KL);
+    constexpr int K = KW * P;
     static_assert(K <= 32, "one 32-cell halo word per side");
-    constexpr int NS = GOL_BYTES_NS;
-    constexpr int NSI = GOL_BYTES_NSI;
-    constexpr int ROW = 64;  // uint32 per LDS row
-    __shared__ uint32_t ring[P - 1][NS][3][ROW];
-    __shared__ uint32_t in_ring[NSI][3][2][256];  // byte rows: [half][lane][16 bytes]
+    constexpr int RPB = 2;            // rows per block: one pair step
+    constexpr int NS = GOL_BYTES_NS;  // (the loops below are unrolled over the NS slots)
+    static_assert(NS == 4, "trip() runs NS steps");
+    constexpr int ROW = 64;  // uint32 per ring row
+    __shared__ uint32_t ring[P - 1][NS][RPB][ROW];
+    __shared__ uint32_t in_ring[NS][RPB][2][256];  // byte rows: [half][lane][16 bytes]
     __shared__ uint2 lut[256];
     __shared__ int ready[P], consumed[P];
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (lds_flag_wr; never read)
@@ -1409,10 +1410,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
     const int R = (int)a.R;
     const int first_in = s0 - K, last_in = s1 + K - 1;
-    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
-    // a pair's range, stretched to s1e so that 3 blocks divide its len + 4K (rows past s1 are
-    // read clamped and never stored: they only feed outputs past s1)
-    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + 2) / 3) * 3 - 4 * K : s1;
+    const int nblk = ((s1 - s0) + 2 * K + RPB - 1) / RPB;
+    constexpr int TRIP = RPB * NS;  // rows per loop trip
+    // a pair's range, stretched to s1e so that TRIP divides its len + 4K (rows past s1 are read
+    // clamped and never stored: they only feed outputs past s1)
+    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + TRIP - 1) / TRIP) * TRIP - 4 * K : s1;
+    const int nclaim = (s1e - s0 + 4 * K) / RPB;  // blocks of the pair (a multiple of NS)
     const int pitch = (int)a.pitch;
     const char *mid_b = reinterpret_cast<const char *>(a.mid);
     const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch;
@@ -1422,17 +1425,13 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
 
-    // stream position t (input row index of this pipeline) -> input row / output row
+    // stream position t -> input row (walking up, dir -1: from s1e + K - 1)
     auto in_row = [&](int t) { return dir >= 0 ? first_in + t : s1e + K - 1 - t; };
-    auto out_row = [&](int t) { return dir >= 0 ? s0 + t - 2 * K : s1e - 1 + 2 * K - t; };
     // wave 0: block b -> an in_ring slot (the slot is an argument: a lambda that captures a
-    // __shared__ array loses the kernel's host-side stub)
-    // Interior blocks (all three rows inside the shard and inside [first_in, last_in]: every block
-    // but the first and last few of a strip) take one row address and step it by a pitch; the
-    // others clamp and pick the row's segment per row (~25 scalar instructions per row, ~150 per
-    // block against the loader's ~400 VALU: same box, 16384^2 bytes +2.4 %)
-    // The loader calls stage_in for blocks 0, 1, 2, ... in order: the first row of the next block
-    // (st_y) and its address (st_g) are carried from call to call.
+    // __shared__ array loses the kernel's host-side stub).  Interior blocks (both rows inside the
+    // shard and inside [first_in, last_in]: every block but the first and last few of a strip) take
+    // one row address, carried from block to block and stepped by a pitch; the others clamp and
+    // pick the row's segment per row (round 4: +2.4 % on 16384^2 bytes over per-row addresses).
     const int in_lo = max(first_in, 0), in_hi = min(last_in, R - 1);
     const int64_t row_step = dir >= 0 ? (int64_t)pitch : -(int64_t)pitch;
     int st_y = in_row(0);
@@ -1440,26 +1439,25 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     auto stage_in = [&](int b, uint32_t (*slot)[2][256]) {
         const int y0 = st_y;
         const char *g = st_g;
-        st_y += dir >= 0 ? 3 : -3;
-        st_g += 3 * row_step;
-        const int ylo = dir >= 0 ? y0 : y0 - 2, yhi = dir >= 0 ? y0 + 2 : y0;
+        st_y += dir >= 0 ? RPB : -RPB;
+        st_g += RPB * row_step;
+        const int ylo = dir >= 0 ? y0 : y0 - (RPB - 1), yhi = dir >= 0 ? y0 + (RPB - 1) : y0;
         if (ylo >= in_lo && yhi <= in_hi) {
 #pragma unroll
-            for (int S = 0; S < 3; ++S) {
+            for (int S = 0; S < RPB; ++S) {
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step), &slot[S][0][0], 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), &slot[S][1][0], 16, 0,
-                                                 0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), &slot[S][1][0], 16, 0, 0);
             }
             return;
         }
 #pragma unroll
-        for (int S = 0; S < 3; ++S) {
-            int y = in_row(3 * b + S);
+        for (int S = 0; S < RPB; ++S) {
+            int y = in_row(RPB * b + S);
             y = y > last_in ? last_in : (y < first_in ? first_in : y);  // past the end: clamped, never stored
             const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
-            const char *g = mid_b + (d + (int64_t)y * pitch) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[S][0][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 16), &slot[S][1][0], 16, 0, 0);
+            const char *gg = mid_b + (d + (int64_t)y * pitch) + lane_off;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg), &slot[S][0][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg + 16), &slot[S][1][0], 16, 0, 0);
         }
     };
     __builtin_amdgcn_s_setprio(1);  // polls drop to 0 (spin_until_ge<true>)
@@ -1478,181 +1476,203 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
-    auto slot_row = [&](int e, int sl, int S) {  // ring e (input of wave e), e >= 1, slot sl
-        return ring_l + (((e - 1) * NS + sl) * 3 + S) * ROW + lane;
-    };
-    // ring slots advance by one per block: running indices instead of b % NS (a division by a
-    // constant, ~6 scalar instructions per use)
-    auto next_slot = [](int x, int n) { return x + 1 == n ? 0 : x + 1; };
+    constexpr int SLOT = RPB * ROW;        // uint32 per hand-off slot
+    constexpr int ISLOT = RPB * 2 * 256;   // uint32 per input slot
+    constexpr int SB = SLOT * 4, RB = ROW * 4, ISB = ISLOT * 4;
     lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
     lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // ring wv+1 ready
     lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // ring wv consumed
+    lds_u32 *const in_base = in_l + lane * 4;
+    lds_u32 *const rd_base = ring_l + (wv - 1) * NS * SLOT + lane;  // ring wv (wv >= 1)
+    lds_u32 *const wr_base = ring_l + wv * NS * SLOT + lane;        // ring wv+1 (wv < P-1)
 
-    Pipe<KX, 1> p;
-    pipe_init(p);
+    PairState<1> st[KW];
+#pragma unroll
+    for (int g = 0; g < KW; ++g) { st[g].a0[0] = 0; st[g].a1[0] = 0; st[g].b0[0] = 0; st[g].b1[0] = 0; st[g].cb[0] = 0; }
     uint32_t alive = 0;
     const uint32_t nrows = (uint32_t)(s1 - s0);
-    // last wave: output row y = out_row(t) stored at voffset st_off + (y - s0) * pitch of ONE
-    // buffer spanning the strip's rows (the host keeps rows x pitch < 2^31): rows before s0
-    // (negative offsets, as unsigned >= 2^32 - 2K * pitch), from s1 on, and a halo lane's 2^31
-    // fall outside it, so no per-row descriptor or branch (as in band_pipe_kernel)
+    // last wave: output row y stored at voffset st_off + (y - s0) * pitch of ONE buffer spanning
+    // the strip's rows (the host keeps rows x pitch < 2^31): rows before s0 (negative offsets, as
+    // unsigned >= 2^32 - 2K * pitch), from s1 on, and a halo lane's 2^31 fall outside it
     const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
         dst_b + (int64_t)s0 * pitch, (short)0, (int)(nrows * (uint32_t)pitch), 0x00020000);
-    int rrel = out_row(0) - s0;  // output row - s0 of stream position 3b + S (wave-uniform)
+    int rrel = dir >= 0 ? -2 * K : s1e - 1 + 2 * K - s0;  // output row - s0 of the next row (wave-uniform)
     const int rstep = dir >= 0 ? 1 : -1;
     uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch;
     const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch;
-    // ready flags count published blocks; the first wave ends the stream with FINAL | blocks,
-    // which every wave passes on after its last block (a paired pipeline learns its block count
-    // only when a claim fails)
-    constexpr int FINAL = 1 << 30;
-    const int nclaim = (s1e - s0 + 4 * K) / 3;  // blocks of the pair
-    const int chunk = a.sm.chunk;
-    auto run = [&](auto role_c) -> bool {
-        constexpr int ROLE = decltype(role_c)::value;  // 0 first, 1 middle, 2 last
-        constexpr int NSTG = ROLE == 0 ? KF : (ROLE == 2 ? KL : KM);
-        int seen_ready = 0, seen_free = 0;
-        int nb = nblk;        // role 0: blocks granted so far
-        uint32_t next = 0;    // role 0, paired: blocks claimed before the pending claim
-        if constexpr (ROLE == 0) {
-            if (dir) {
-                // lane 0 claims (see band_pipe_kernel); a claim's return is waited for where it
-                // is used
-                uint32_t c0 = 0;
-                if (lane == 0) c0 = atomicAdd(ctr, (uint32_t)chunk);
-                c0 = __builtin_amdgcn_readfirstlane(c0);
-                nb = c0 >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c0);
-                if (nb == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);  // prefetched claim
-            }
+    // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit takes its shift
+    // mod 32), unpack through the LUT, store, count
+    auto emit = [&](uint32_t w) {
+        const uint32_t nxw = from_upper_lane(w);
+        const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nxw, w, K % 32) : nxw;
+        uint2 e[4];
 #pragma unroll
-            for (int i = 0; i < NSI - 1; ++i) stage_in(i, in_ring[i]);
+        for (int q = 0; q < 4; ++q) e[q] = lut[(o >> (8 * q)) & 0xFF];
+        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[0].x, e[0].y, e[1].x, e[1].y}, strip_rs, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[2].x, e[2].y, e[3].x, e[3].y}, strip_rs, voff + 16u, 0, 0);
+        if constexpr (COUNT) {
+            const uint32_t c = __popc(o) + alive;
+            alive = (uint32_t)rrel < nrows ? c : alive;
         }
-        // Readers (waves 1 .. P-1): block b+1's rows are read at the end of block b (spinning
-        // there for its flag if needed) and waited for at the top of block b+1; a middle wave
-        // publishes "blocks < b ready" right after that wait, which also covers its writes of
-        // block b-1 (a wave's LDS operations complete in order), so no wave waits for its own
-        // writes.  The first wave publishes after its block's compute (its writes of the
-        // previous block are long done by then).
-        uint32_t nx[3] = {0, 0, 0};
-        bool more = true;
-        if constexpr (ROLE != 0) {
-            if (seen_ready < 1) {
-                seen_ready = spin_until_ge<true>(ready_l + wv, 1);
+        voff += vstep;
+        rrel += rstep;
+    };
+    constexpr int FINAL = 1 << 30;  // ready flag = FINAL + blocks: the stream has ended
+    uint32_t pending = 0;  // the loader's claim in flight (paired)
+    if (wv == 0 && dir && lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
+    // block 0's rows read to completion here (the compiler copies loop-carried registers on loop
+    // entry, which must not happen while a read is in flight).  The loader's next block: four
+    // 16-byte halves; a reader's: two words.
+    v4u32 nb0, nb1, nb2, nb3;  // loader
+    uint32_t nw0 = 0, nw1 = 0;  // readers
+    int seen_ready = 0, seen_free = 0;
+    if (wv == 0) {
+        stage_in(0, in_ring[0]);
+        stage_in(1, in_ring[1]);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block 0 landed (the claim before it too)
+        nb0 = lds_rd128_issue_o<0>(in_base);
+        nb1 = lds_rd128_issue_o<1024>(in_base);
+        nb2 = lds_rd128_issue_o<2048>(in_base);
+        nb3 = lds_rd128_issue_o<3072>(in_base);
+        lds_settle<0>(nb0);
+        lds_settle<0>(nb1);
+        lds_settle<0>(nb2);
+        lds_settle<0>(nb3);
+    } else {
+        seen_ready = spin_until_ge<true>(ready_l + wv, 1);
+        if (seen_ready < 0) {
+            raise_error(a.err, GOLK_ERR_SPIN);
+            return;
+        }
+        nw0 = lds_rd32(rd_base);
+        nw1 = lds_rd32(rd_base + ROW);
+    }
+    bool more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
+    auto step = [&](int b, auto u_c, auto role_c, auto dyn_c, auto skip_c) -> bool {
+        constexpr int US = decltype(u_c)::value;
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool DYN = decltype(dyn_c)::value;
+        constexpr bool SKIP = decltype(skip_c)::value;  // a fill block: no rule (see run)
+        constexpr bool LAST = ROLE == 2;
+        constexpr int NXT = (US + 1) % NS;
+        uint32_t r0, r1;
+        // block b's rows, the youngest LDS operations of this wave: once they are in, so are
+        // block b-1's row writes, and both flags can go out at once
+        if constexpr (ROLE == 0) {
+            lds_settle<0>(nb0);
+            lds_settle<0>(nb1);
+            lds_settle<0>(nb2);
+            lds_settle<0>(nb3);
+            r0 = pack32_ff(uint4{nb0.x, nb0.y, nb0.z, nb0.w}, uint4{nb1.x, nb1.y, nb1.z, nb1.w});
+            r1 = pack32_ff(uint4{nb2.x, nb2.y, nb2.z, nb2.w}, uint4{nb3.x, nb3.y, nb3.z, nb3.w});
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nw0), "+v"(nw1)::"memory");
+            r0 = nw0;
+            r1 = nw1;
+            lds_flag_wr(cns_addr, b + 1);  // block b's slot is free
+        }
+        if constexpr (!LAST) lds_flag_wr(rdy_addr, b);  // blocks < b are in ring wv+1
+        if constexpr (!SKIP) {
+#pragma unroll
+            for (int g = 0; g < KW; ++g) spstage(st[g], r0, r1);
+        }
+        if constexpr (LAST) {
+            emit(r0);
+            emit(r1);
+        } else {
+            if (seen_free < b + 1 - NS) {  // slot b % NS: block b - NS consumed
+                seen_free = spin_until_ge<true>(consumed_l + wv + 1, b + 1 - NS);
+                if (seen_free < 0) return false;
+            }
+            asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(wr_base), "v"(r0), "i"(US * SB) : "memory");
+            asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(wr_base), "v"(r1), "i"(US * SB + RB) : "memory");
+        }
+        // block b+1's rows: read now, waited for at the next block's start
+        if constexpr (ROLE == 0) {
+            stage_in(b + 2, in_ring[(US + 2) % NS]);  // refills block b-2's slot (clamped past the end)
+            // block b+1 landed, b+2 in flight (4 loads; and, paired, at US 1 the claim issued at US 0)
+            if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            if constexpr (DYN && US == 0) {
+                if (lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
+            }
+            nb0 = lds_rd128_issue_o<NXT * ISB>(in_base);
+            nb1 = lds_rd128_issue_o<NXT * ISB + 1024>(in_base);
+            nb2 = lds_rd128_issue_o<NXT * ISB + 2048>(in_base);
+            nb3 = lds_rd128_issue_o<NXT * ISB + 3072>(in_base);
+        } else {
+            // the next block exists unless the writer's flag says the stream ended before it
+            if (seen_ready < b + 2) {
+                seen_ready = spin_until_ge<true>(ready_l + wv, b + 2);
                 if (seen_ready < 0) return false;
             }
-            more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
-            if (more) lds_rd32x3_issue(slot_row(wv, 0, 0), nx);
+            more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(nw0) : "v"(rd_base), "i"(NXT * SB) : "memory");
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(nw1) : "v"(rd_base), "i"(NXT * SB + RB) : "memory");
         }
+        return true;
+    };
+    auto grant = [&](uint32_t c) { return c >= (uint32_t)nclaim ? 0 : NS; };
+    auto trip = [&](int b, auto role_c, auto dyn_c, auto skip_c) -> bool {
+        return step(b, std::integral_constant<int, 0>(), role_c, dyn_c, skip_c) &&
+               step(b + 1, std::integral_constant<int, 1>(), role_c, dyn_c, skip_c) &&
+               step(b + 2, std::integral_constant<int, 2>(), role_c, dyn_c, skip_c) &&
+               step(b + 3, std::integral_constant<int, 3>(), role_c, dyn_c, skip_c);
+    };
+    auto run = [&](auto role_c, auto dyn_c) -> bool {
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool DYN = decltype(dyn_c)::value;
+        int nb = DYN ? 0 : (nblk + NS - 1) / NS * NS;
         int b = 0;
-        int wsl = 0, rsl = 1 % NS, isl = 0;  // b % NS, (b + 1) % NS, b % NSI
-        const int g0 = ROLE == 0 ? 0 : (ROLE == 2 ? K - KL : KF + (wv - 1) * KM);  // first stage of this wave
-        const int skip_b = (2 * g0) / 3;  // blocks 0 .. skip_b-1 end before step 2 g0
-        for (;; ++b, wsl = next_slot(wsl, NS), rsl = next_slot(rsl, NS), isl = next_slot(isl, NSI)) {
-            uint32_t w3[3];
+        // Fill blocks (band_pipe_kernel's rule): a wave whose first stage is g0 = KW * wv passes
+        // the blocks before step 2 g0 on without the rule, whole loop trips of them
+        if constexpr (ROLE != 0) {
+            const int nskip = KW * wv;
+            for (; b + NS <= nskip; b += NS) {
+                if (!more) break;
+                if (!trip(b, role_c, dyn_c, std::true_type())) return false;
+            }
+        }
+        for (;; b += NS) {
             if constexpr (ROLE == 0) {
-                if (b >= nb) {
-                    if (!dir || nb % chunk != 0 || nb == 0) break;
-                    const uint32_t c = __builtin_amdgcn_readfirstlane(next);
-                    const int g = c >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c);
-                    if (g == 0) break;
-                    nb += g;
-                    if (g == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);
-                }
-                // block b landed (blocks b+1 .. b+NSI-2 may still be in flight: 6 loads each)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSI - 2) * 6) : "memory");
-                v4u32 raw[6];
-                lds_rd_block6(in_l + isl * (3 * 2 * 256) + lane * 4, raw);
-#pragma unroll
-                for (int S = 0; S < 3; ++S)
-                    w3[S] = pack32_ff(uint4{raw[2 * S].x, raw[2 * S].y, raw[2 * S].z, raw[2 * S].w},
-                                      uint4{raw[2 * S + 1].x, raw[2 * S + 1].y, raw[2 * S + 1].z, raw[2 * S + 1].w});
-                // refill block b-1's slot (read to completion in the previous trip; clamped past the end)
-                stage_in(b + NSI - 1, in_ring[isl == 0 ? NSI - 1 : isl - 1]);
+                if constexpr (DYN) nb += grant(__builtin_amdgcn_readfirstlane(pending));
+                if (b >= nb) break;
             } else {
                 if (!more) break;
-                lds_wait3(nx);  // block b's rows (and every older LDS operation of this wave)
-                w3[0] = nx[0]; w3[1] = nx[1]; w3[2] = nx[2];
-                lds_flag_wr(cns_addr, b + 1);
-                if constexpr (ROLE == 1) lds_flag_wr(rdy_addr, b);  // blocks < b: written and complete
             }
-            // Fill rows: stage g's input is valid from stream step 2g on (each stage needs the two
-            // rows before), and only its outputs from step 2g + 2 on are ever used, so a wave whose
-            // first stage is g0 skips the blocks that end before step 2 g0 (their rows pass on as
-            // they are; its pipe state is stale until step 2 g0, where nothing needs it yet).
-            if (b >= skip_b) sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
-            if constexpr (ROLE == 2) {
-                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit takes
-                // its shift mod 32), unpack row by row through the LUT (all 12 reads ahead of the
-                // stores measured 0.9 % slower)
-                uint32_t o[3];
-                uint2 e[3][4];
-#pragma unroll
-                for (int S = 0; S < 3; ++S) {
-                    const uint32_t nxw = from_upper_lane(w3[S]);
-                    o[S] = K % 32 ? __builtin_amdgcn_alignbit(nxw, w3[S], K % 32) : nxw;
-                }
-#pragma unroll
-                for (int S = 0; S < 3; ++S) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) e[S][q] = lut[(o[S] >> (8 * q)) & 0xFF];
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[S][0].x, e[S][0].y, e[S][1].x, e[S][1].y}, strip_rs, voff, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[S][2].x, e[S][2].y, e[S][3].x, e[S][3].y}, strip_rs, voff + 16u, 0, 0);
-                    if constexpr (COUNT)
-                        alive += bitop3<0x80>((uint32_t)__popc(o[S]), st_mask, (uint32_t)rrel < nrows ? 0xFFFFFFFFu : 0u);
-                    voff += vstep;
-                    rrel += rstep;
-                }
-            } else {
-                if constexpr (ROLE == 0) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // block b-1's writes
-                    lds_flag_wr(rdy_addr, b);
-                }
-                if (seen_free < b + 1 - NS) {
-                    seen_free = spin_until_ge<true>(consumed_l + wv + 1, b + 1 - NS);
-                    if (seen_free < 0) return false;
-                }
-#pragma unroll
-                for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, wsl, S), (int)w3[S]);
-            }
-            if constexpr (ROLE != 0) {
-                if (seen_ready < b + 2) {
-                    seen_ready = spin_until_ge<true>(ready_l + wv, b + 2);
-                    if (seen_ready < 0) return false;
-                }
-                more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
-                if (more) lds_rd32x3_issue(slot_row(wv, rsl, 0), nx);
-            }
+            if (!trip(b, role_c, dyn_c, std::false_type())) return false;
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last block's reads of the next slot
         if constexpr (ROLE != 2) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_flag_wr(rdy_addr, FINAL + b);
         }
-        if constexpr (ROLE == 0) {
-            if (dir && lane == 0) {
-                // this pipeline's claims are over (none in flight): the second of the pair to get
-                // here zeroes the counters for the next launch
-                if (atomicAdd(ctr + 1, 1u) == 1u) {
-                    atomicExch(ctr, 0u);
-                    atomicExch(ctr + 1, 0u);
-                }
+        if constexpr (ROLE == 0 && DYN) {
+            if (lane == 0 && atomicAdd(ctr + 1, 1u) == 1u) {  // both loaders' claims are over
+                atomicExch(ctr, 0u);
+                atomicExch(ctr + 1, 0u);
             }
         }
         return true;
     };
+    auto run_role = [&](auto role_c) -> bool {
+        return dir ? run(role_c, std::true_type()) : run(role_c, std::false_type());
+    };
     bool ok;
-    if (wv == 0) ok = run(std::integral_constant<int, 0>());
-    else if (wv == P - 1) ok = run(std::integral_constant<int, 2>());
-    else ok = run(std::integral_constant<int, 1>());
+    if (wv == 0) ok = run_role(std::integral_constant<int, 0>());
+    else if (wv == P - 1) ok = run_role(std::integral_constant<int, 2>());
+    else ok = run_role(std::integral_constant<int, 1>());
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input blocks staged past the end
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
+    alive &= st_mask;  // halo lanes' rows are not this group's
     if (COUNT && wv == P - 1) slot_add(a.slots, alive);
 }
 
-#ifndef GOL_BYTES_PIPE_STAGES
-#define GOL_BYTES_PIPE_STAGES 4, 4, 4
+#ifndef GOL_BYTES_PIPE_KW
+#define GOL_BYTES_PIPE_KW 4
 #define GOL_BYTES_PIPE_P 8
 #endif
-#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
+#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_KW, GOL_BYTES_PIPE_P, count>)
 
 #ifdef GOL_TU_BYTES_PIPE
 }  // namespace golk
@@ -2449,7 +2469,7 @@ static bool band_rank_map(int64_t rows, int64_t ngroups, int64_t pitch, int cus,
     if (cus <= 0 || slots <= 0) return false;
     StripMap m{};
     if (!rank_split(rows, ngroups, cus, (int)(slots / cus), BAND_PIPE_RANK_W, 8 * KW * P, 1024, m, GOL_BAND_PAIRED,
-                    claims, 3, BAND_RANK_ROUNDS))
+                    claims, GOL_BAND_NS, BAND_RANK_ROUNDS))
         return false;
     if ((int64_t)m.period * pitch * 4 >= (int64_t(1) << 31)) return false;  // a range's stores: one 32-bit buffer
     sm = m;
@@ -2457,16 +2477,15 @@ static bool band_rank_map(int64_t rows, int64_t ngroups, int64_t pitch, int cus,
 }
 
 // band_pipe_kernel lives in its own translation unit (gol_band_pipe.hip: another scheduler)
-const void *golk_band_pipe_fn(bool contig, bool count, bool rowf);
-hipError_t golk_band_pipe_launch(bool contig, bool count, bool rowf, unsigned nwg, const BitsArgs &a, hipStream_t s);
+const void *golk_band_pipe_fn(bool contig, bool count);
+hipError_t golk_band_pipe_launch(bool contig, bool count, unsigned nwg, const BitsArgs &a, hipStream_t s);
 
 // k = 12 on the band layout: 4 waves x 3 stages (band_pipe_kernel).
 static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool auto_strip)
 {
     constexpr int KW = GOL_BAND_KW, P = GOL_BAND_P;
     const bool count = a.slots != nullptr;
-    const void *kf = golk_band_pipe_fn(contig, count, false);
-    // (the row-flag instantiations have the same resources: one occupancy query serves both)
+    const void *kf = golk_band_pipe_fn(contig, count);
     int64_t nwg = 0;
     const int cus = device_cus();
     const int64_t slots = resident_workgroups(kf, 64 * P);
@@ -2489,11 +2508,7 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
             nwg = a.sm.tail_l + a.ngroups * ((tail_rows + ts - 1) / ts);
         }
     }
-#ifndef GOL_BAND_RANK_ROWF
-#define GOL_BAND_RANK_ROWF 1
-#endif
-    // one-round launch: row-grain hand-off flags
-    return golk_band_pipe_launch(contig, count, a.sm.ranked && GOL_BAND_RANK_ROWF, (unsigned)nwg, a, s);
+    return golk_band_pipe_launch(contig, count, (unsigned)nwg, a, s);
 }
 
 hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32_t *bot, uint32_t *dst, int64_t R,
@@ -2547,7 +2562,7 @@ double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int64_t pitch, int 
 {
     if (!band || dw != 4 || k != 12 || rows <= 0) return 1e9;
     const int64_t ngroups = (Wd + band_useful_words(k, dw) - 1) / band_useful_words(k, dw);
-    const int64_t slots = resident_workgroups(golk_band_pipe_fn(true, true, false), 64 * GOL_BAND_P);
+    const int64_t slots = resident_workgroups(golk_band_pipe_fn(true, true), 64 * GOL_BAND_P);
     if (slots <= 0) return 1e9;
     StripMap sm{};
     if (strip <= 0 && band_rank_map(rows, ngroups, pitch, device_cus(), slots, nullptr, sm)) return 1.0;
@@ -2621,7 +2636,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         const int64_t max_rows = std::max<int64_t>(1, ((int64_t(1) << 31) - 1) / pitch - 1);
         if (strip <= 0 && cus > 0 &&
             rank_split(rows, a.ngroups, cus, (int)std::min<int64_t>(GOL_BYTES_PER_CU, slots / cus), BYTES_PIPE_RANK_W,
-                       2 * k, 1024, a.sm, claims != nullptr, claims, 4) && a.sm.period <= max_rows) {
+                       2 * k, 1024, a.sm, claims != nullptr, claims, GOL_BYTES_NS) && a.sm.period <= max_rows) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
             a.sm = StripMap{};
