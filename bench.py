@@ -264,9 +264,10 @@ def roofline(kind, launch_ms, cell_updates, pmc, pmc_note):
                   "frac_at_profile_clock": round(ach / (VALU_PEAK_GINST / 2.4 * pmc["clock_GHz"]), 4)
                   if pmc.get("clock_GHz") else None,
                   "cell_updates_per_valu_lane_op": round(cell_updates / (valu * 64), 3),
-                  "note": "VALU issue of the kernel's own instruction stream; since round 3 a band-layout "
-                          "generation is 9 logic ops per 32 cells (10 before, DESIGN.md §4.1), so the same "
-                          "frac means ~10 % more cell-updates/s"})
+                  "note": "VALU issue of the kernel's own instruction stream; since round 5 a band-layout "
+                          "generation is 8 logic ops per 32 cells (two output rows share their middle rows' "
+                          "sum; 9 in rounds 3-4, 10 before: DESIGN.md §4.1, §4.1b), so the same frac means "
+                          "~12 % more cell-updates/s than in round 4"})
     else:  # no PMC profile of this kernel build: only the HBM side can be stated (None without traffic)
         r.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": hbm["frac"]})
