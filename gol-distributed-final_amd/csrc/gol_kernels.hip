@@ -660,6 +660,18 @@ __device__ __forceinline__ void lds_wr128_o(lds_u32 *p, v4u32 v)
 {
     asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(p), "v"(v), "i"(OFF) : "memory");
 }
+template <int OFF>
+__device__ __forceinline__ void lds_wr32_o(lds_u32 *p, uint32_t v)
+{
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(p), "v"(v), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_rd32_issue_o(const lds_u32 *p)
+{
+    uint32_t r;
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(p), "i"(OFF) : "memory");
+    return r;
+}
 // Flag write without an exec mask: lane 0's address is the flag, the other lanes write their
 // own scratch word (one ds_write, no saveexec / branch around it).
 __device__ __forceinline__ void lds_flag_wr(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
@@ -869,7 +881,27 @@ band_pipe_kernel(BitsArgs a)
 
     // wave 0: block b -> in_ring[b % NS] (global_load_lds).  The slot is an argument: a lambda
     // that captures a __shared__ array silently loses the kernel's host-side stub.
+    // Interior blocks (both rows inside [first_in, last_in] and, unless CONTIG, inside the shard's
+    // own rows: every block but the first and last few of a strip) take the row address carried
+    // from the previous block (uniform) plus the lane's offset; the others clamp and pick the row's
+    // segment per row.  stage_in is called for blocks 0, 1, 2, ... in order.
+    const int in_lo = CONTIG ? first_in : max(first_in, 0), in_hi = CONTIG ? last_in : min(last_in, R - 1);
+    const int64_t row_step = dir >= 0 ? (int64_t)pitch_b : -(int64_t)pitch_b;
+    int st_y = dir >= 0 ? first_in : s1e + K - 1;  // first row of the next block
+    const char *st_row = mid_b + (int64_t)st_y * pitch_b;  // its address (used when interior)
     auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
+        const int y0 = st_y;
+        const char *g0 = st_row;
+        st_y += dir >= 0 ? RPB : -RPB;
+        st_row += RPB * row_step;
+        const int ylo = dir >= 0 ? y0 : y0 - (RPB - 1), yhi = dir >= 0 ? y0 + (RPB - 1) : y0;
+        if (ylo >= in_lo && yhi <= in_hi) {
+#pragma unroll
+            for (int s = 0; s < RPB; ++s)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g0 + s * row_step + lane_off), &slot[s][0], 16, 0,
+                                                 GOL_BAND_LOAD_AUX);
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < RPB; ++s) {
             const int t = RPB * b + s;  // stream position
@@ -1339,95 +1371,78 @@ __global__ void __launch_bounds__(256) bytes_blocked_kernel(BytesKArgs a)
     if (a.slots) slot_add(a.slots, alive);
 }
 
-// Byte board, split pipeline: K = KW * P turns per launch, P waves per workgroup on one
-// column group of 62 words (32 cells per lane, standard bit layout in registers, shifted
-// frame), KW stages per wave, 3-row blocks handed on through LDS rings (256 B per row) with
-// the flag protocol of band_pipe_kernel.  Wave 0 loads and packs the bytes, wave P-1
-// realigns, unpacks and stores them.  One 32-cell word per lane covers K <= 32 columns of
-// halo, so K = 32 costs no more lanes than K = 16, and the 16384^2 board gets P waves per
-// column group instead of one (the one-wave kernel runs at ~1 wave per SIMD there).
-// Rows S = 0, 1, 2 of one ring slot (ROW = 64 uint32 apart), read and waited for together.
-__device__ __forceinline__ void lds_rd32x3(const lds_u32 *p, uint32_t (&r)[3])
+// f(integral_constant<0>), .., f(integral_constant<N-1>), unrolled
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F &&f)
 {
-    asm volatile(
-        "ds_read_b32 %0, %3\n\t"
-        "ds_read_b32 %1, %3 offset:256\n\t"
-        "ds_read_b32 %2, %3 offset:512\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
-        : "v"(p)
-        : "memory");
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>());
+        static_for<N, I + 1>(f);
+    }
 }
 
-// The same three reads without the wait, and the wait (the values are in-out operands, so no
-// use of them moves above it).
-__device__ __forceinline__ void lds_rd32x3_issue(const lds_u32 *p, uint32_t (&r)[3])
+// Byte board, split pipeline: K = KW * P turns per launch, P waves per workgroup on one
+// column group of 62 words (32 cells per lane, standard bit layout in registers, shifted
+// frame), KW stages per wave, blocks of 4 rows (two pair steps, as band_pipe_kernel's, run as a
+// wavefront: the second pair one stage behind the first, two independent pair steps in flight
+// per stage step -- one 32-cell word per lane is otherwise one dependent chain) handed on
+// through LDS rings of NS slots (256 B per row) with band_pipe_kernel's flag protocol and loop
+// shape: one loop per role, unrolled over the NS slots (every LDS address a register plus an
+// immediate, no slot arithmetic, no per-block branch for the fill blocks).  Wave 0 stages its
+// input blocks HBM -> LDS with global_load_lds and packs 32 bytes per lane into one word with
+// v_dot4_i32_i8; wave P-1 realigns (after 32 stages the frame shift is exactly one word),
+// unpacks through a 2 KiB LDS table (byte -> 8 bytes of 0x00 / 0xFF) and stores the strip
+// through one buffer descriptor with a running offset.  One 32-cell word per lane covers K <= 32
+// columns of halo, so K = 32 costs no more lanes than K = 16.
+// (Round 4's form -- 3-row blocks, one block per loop trip with running slot indices and a
+// per-block fill branch -- spent 0.44 scalar instructions per VALU: DESIGN.md §4.4.)
+//
+// Shifted-frame pair step: pstage's circuit on this frame.  A row's 3-sum at bit p is
+// c[p] + c[p-1] + c[p-2] (centred on p-1: the neighbour from the lower lane by one DPP, two
+// v_alignbit), the cell is c[p-1]; every stage moves the frame one bit to the left.
+__device__ __forceinline__ void spstage(PairState<1> &s, uint32_t &r0, uint32_t &r1)
 {
-    asm volatile(
-        "ds_read_b32 %0, %3\n\t"
-        "ds_read_b32 %1, %3 offset:256\n\t"
-        "ds_read_b32 %2, %3 offset:512"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
-        : "v"(p)
-        : "memory");
-}
-__device__ __forceinline__ void lds_wait3(uint32_t (&r)[3])
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2])::"memory");
+    const uint32_t w0 = from_lower_lane(r0), w1 = from_lower_lane(r1);
+    const uint32_t l0 = __builtin_amdgcn_alignbit(r0, w0, 31), m0 = __builtin_amdgcn_alignbit(r0, w0, 30);
+    const uint32_t l1 = __builtin_amdgcn_alignbit(r1, w1, 31), m1 = __builtin_amdgcn_alignbit(r1, w1, 30);
+    const uint32_t c0 = bitop3<TT_XOR3>(l0, r0, m0), c1 = bitop3<TT_MAJ>(l0, r0, m0);
+    const uint32_t d0 = bitop3<TT_XOR3>(l1, r1, m1), d1 = bitop3<TT_MAJ>(l1, r1, m1);
+    const uint32_t k = s.b0[0] & c0;
+    const uint32_t p0 = s.b0[0] ^ c0;
+    const uint32_t p1 = bitop3<TT_XOR3>(s.b1[0], c1, k);
+    const uint32_t p2 = bitop3<TT_MAJ>(s.b1[0], c1, k);
+    r0 = pair_tail(p0, p1, p2, s.a0[0], s.a1[0], s.cb[0]);  // row 2m-1: its cell = c[p-1] of x_2m-1
+    r1 = pair_tail(p0, p1, p2, d0, d1, l0);                 // row 2m: its cell = c[p-1] of x_2m
+    s.a0[0] = c0;
+    s.a1[0] = c1;
+    s.b0[0] = d0;
+    s.b1[0] = d1;
+    s.cb[0] = l1;
 }
 
 #ifndef GOL_BYTES_PER_CU
 #define GOL_BYTES_PER_CU 3  // workgroups per CU of a one-round launch
 #endif
-// Ring slots per inter-wave ring of the byte pipeline: 4 measured +1.5 % over 3 (16384^2, same
-// box), 6 (with NSI = 3 below, which alone cost 0.6 %, and one flag-scratch row for all waves:
-// 53 KiB per workgroup, still 3 per CU) +1.3-3 % over 4; role order reversed on each SIMD (the
-// older wave of a SIMD the downstream one) -5 %; with the hand-off software-pipelined (reads one block ahead, no wait for own writes)
-// the byte pipeline ran within 2 % of the blocking version, and 4 x 8-stage waves equal to 8 x 4:
-// at ~0.45-0.49 of the VALU issue roof neither the hand-off nor the HBM streams (no loads and
-// no stores: +10 %) bound it.
+// Ring slots of the byte pipeline: NS hand-off slots of 4 rows between the waves, NSI input slots
+// of the first wave (2 blocks in flight); the role loops are unrolled over NS (NSI divides it)
 #ifndef GOL_BYTES_NS
-#define GOL_BYTES_NS 6
+#define GOL_BYTES_NS 3
 #endif
-// Input ring of the byte pipeline's first wave: blocks of 3 byte rows staged HBM -> LDS with
-// global_load_lds (no VGPRs), NSI - 1 blocks in flight while the wave packs and computes one.
 #ifndef GOL_BYTES_NSI
 #define GOL_BYTES_NSI 3
 #endif
-// The six 16-byte halves of one input block (row S: lo at S * 2 KiB, hi at S * 2 KiB + 1 KiB,
-// lane * 16 within each), read and waited for together.
-__device__ __forceinline__ void lds_rd_block6(const lds_u32 *p, v4u32 (&r)[6])
+template <int KW, int P, bool COUNT>
+__global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 8))) bytes_pipe_kernel(BytesKArgs a)
 {
-    asm volatile(
-        "ds_read_b128 %0, %6\n\t"
-        "ds_read_b128 %1, %6 offset:1024\n\t"
-        "ds_read_b128 %2, %6 offset:2048\n\t"
-        "ds_read_b128 %3, %6 offset:3072\n\t"
-        "ds_read_b128 %4, %6 offset:4096\n\t"
-        "ds_read_b128 %5, %6 offset:5120\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5])
-        : "v"(p)
-        : "memory");
-}
-// 1-D grid of work items (work_item).  P waves of one column group: wave 0 loads its input
-// byte rows (one 3-row block ahead, in registers) and packs them with v_dot4_i32_i8, runs KF
-// stages and hands the block on; waves 1 .. P-2 run KM stages each; wave P-1 runs KL stages,
-// realigns the frame, unpacks through a 2 KiB LDS table (byte value -> 8 bytes of 0x00 / 0xFF)
-// and stores.  The first and last waves carry the byte conversion, so they get fewer stages
-// (a wave that is busy when its consumer wants the next block sets the pipeline's rate).
-// One loop per role (no role branches inside the loop).
-template <int KF, int KM, int KL, int P, bool COUNT>
-__global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
-{
-    constexpr int K = KF + (P - 2) * KM + KL;
-    constexpr int KX = KM > KF ? (KM > KL ? KM : KL) : (KF > KL ? KF : KL);
+    constexpr int K = KW * P;
     static_assert(K <= 32, "one 32-cell halo word per side");
-    constexpr int NS = GOL_BYTES_NS;
+    constexpr int RPB = 4;            // rows per block: two pair steps
+    constexpr int NS = GOL_BYTES_NS;  // (the loops below are unrolled over the NS slots)
     constexpr int NSI = GOL_BYTES_NSI;
-    constexpr int ROW = 64;  // uint32 per LDS row
-    __shared__ uint32_t ring[P - 1][NS][3][ROW];
-    __shared__ uint32_t in_ring[NSI][3][2][256];  // byte rows: [half][lane][16 bytes]
+    static_assert(NS % NSI == 0 && NSI >= 3, "input slots: 2 blocks in flight, one being read");
+    constexpr int ROW = 64;  // uint32 per ring row
+    __shared__ uint32_t ring[P - 1][NS][RPB][ROW];
+    __shared__ uint32_t in_ring[NSI][RPB][2][256];  // byte rows: [half][lane][16 bytes]
     __shared__ uint2 lut[256];
     __shared__ int ready[P], consumed[P];
     __shared__ int flag_scratch[64];  // dummy target of lanes 1..63's flag writes (lds_flag_wr; never read)
@@ -1443,10 +1458,12 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const bool writer = lane >= 1 && lane <= 62 && col_raw < a.Wd;
     const int R = (int)a.R;
     const int first_in = s0 - K, last_in = s1 + K - 1;
-    const int nblk = ((s1 - s0) + 2 * K + 2) / 3;
-    // a pair's range, stretched to s1e so that 3 blocks divide its len + 4K (rows past s1 are
-    // read clamped and never stored: they only feed outputs past s1)
-    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + 2) / 3) * 3 - 4 * K : s1;
+    const int nblk = ((s1 - s0) + 2 * K + RPB - 1) / RPB;
+    constexpr int TRIP = RPB * NS;  // rows per loop trip
+    // a pair's range, stretched to s1e so that TRIP divides its len + 4K (rows past s1 are read
+    // clamped and never stored: they only feed outputs past s1)
+    const int s1e = dir ? s0 + ((s1 - s0 + 4 * K + TRIP - 1) / TRIP) * TRIP - 4 * K : s1;
+    const int nclaim = (s1e - s0 + 4 * K) / RPB;  // blocks of the pair (a multiple of NS)
     const int pitch = (int)a.pitch;
     const char *mid_b = reinterpret_cast<const char *>(a.mid);
     const int64_t top_d = (reinterpret_cast<const char *>(a.top) - mid_b) + (int64_t)K * pitch;
@@ -1456,17 +1473,13 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     const uint32_t st_off = writer ? lane_off : 0x80000000u;
     const uint32_t st_mask = writer ? 0xFFFFFFFFu : 0u;
 
-    // stream position t (input row index of this pipeline) -> input row / output row
+    // stream position t -> input row (walking up, dir -1: from s1e + K - 1)
     auto in_row = [&](int t) { return dir >= 0 ? first_in + t : s1e + K - 1 - t; };
-    auto out_row = [&](int t) { return dir >= 0 ? s0 + t - 2 * K : s1e - 1 + 2 * K - t; };
     // wave 0: block b -> an in_ring slot (the slot is an argument: a lambda that captures a
-    // __shared__ array loses the kernel's host-side stub)
-    // Interior blocks (all three rows inside the shard and inside [first_in, last_in]: every block
-    // but the first and last few of a strip) take one row address and step it by a pitch; the
-    // others clamp and pick the row's segment per row (~25 scalar instructions per row, ~150 per
-    // block against the loader's ~400 VALU: same box, 16384^2 bytes +2.4 %)
-    // The loader calls stage_in for blocks 0, 1, 2, ... in order: the first row of the next block
-    // (st_y) and its address (st_g) are carried from call to call.
+    // __shared__ array loses the kernel's host-side stub).  Interior blocks (both rows inside the
+    // shard and inside [first_in, last_in]: every block but the first and last few of a strip) take
+    // one row address, carried from block to block and stepped by a pitch; the others clamp and
+    // pick the row's segment per row (round 4: +2.4 % on 16384^2 bytes over per-row addresses).
     const int in_lo = max(first_in, 0), in_hi = min(last_in, R - 1);
     const int64_t row_step = dir >= 0 ? (int64_t)pitch : -(int64_t)pitch;
     int st_y = in_row(0);
@@ -1474,26 +1487,25 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     auto stage_in = [&](int b, uint32_t (*slot)[2][256]) {
         const int y0 = st_y;
         const char *g = st_g;
-        st_y += dir >= 0 ? 3 : -3;
-        st_g += 3 * row_step;
-        const int ylo = dir >= 0 ? y0 : y0 - 2, yhi = dir >= 0 ? y0 + 2 : y0;
+        st_y += dir >= 0 ? RPB : -RPB;
+        st_g += RPB * row_step;
+        const int ylo = dir >= 0 ? y0 : y0 - (RPB - 1), yhi = dir >= 0 ? y0 + (RPB - 1) : y0;
         if (ylo >= in_lo && yhi <= in_hi) {
 #pragma unroll
-            for (int S = 0; S < 3; ++S) {
+            for (int S = 0; S < RPB; ++S) {
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step), &slot[S][0][0], 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), &slot[S][1][0], 16, 0,
-                                                 0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), &slot[S][1][0], 16, 0, 0);
             }
             return;
         }
 #pragma unroll
-        for (int S = 0; S < 3; ++S) {
-            int y = in_row(3 * b + S);
+        for (int S = 0; S < RPB; ++S) {
+            int y = in_row(RPB * b + S);
             y = y > last_in ? last_in : (y < first_in ? first_in : y);  // past the end: clamped, never stored
             const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
-            const char *g = mid_b + (d + (int64_t)y * pitch) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[S][0][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 16), &slot[S][1][0], 16, 0, 0);
+            const char *gg = mid_b + (d + (int64_t)y * pitch) + lane_off;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg), &slot[S][0][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg + 16), &slot[S][1][0], 16, 0, 0);
         }
     };
     __builtin_amdgcn_s_setprio(1);  // polls drop to 0 (spin_until_ge<true>)
@@ -1512,181 +1524,227 @@ __global__ void __launch_bounds__(64 * P) bytes_pipe_kernel(BytesKArgs a)
     lds_u32 *const in_l = (lds_u32 *)&in_ring[0][0][0][0];
     lds_u32 *const ready_l = (lds_u32 *)&ready[0];
     lds_u32 *const consumed_l = (lds_u32 *)&consumed[0];
-    auto slot_row = [&](int e, int sl, int S) {  // ring e (input of wave e), e >= 1, slot sl
-        return ring_l + (((e - 1) * NS + sl) * 3 + S) * ROW + lane;
-    };
-    // ring slots advance by one per block: running indices instead of b % NS (a division by a
-    // constant, ~6 scalar instructions per use)
-    auto next_slot = [](int x, int n) { return x + 1 == n ? 0 : x + 1; };
+    constexpr int SLOT = RPB * ROW;        // uint32 per hand-off slot
+    constexpr int ISLOT = RPB * 2 * 256;   // uint32 per input slot
+    constexpr int SB = SLOT * 4, RB = ROW * 4, ISB = ISLOT * 4;
     lds_u32 *const scratch = (lds_u32 *)&flag_scratch[0] + lane;
     lds_u32 *const rdy_addr = lane == 0 ? ready_l + wv + 1 : scratch;  // ring wv+1 ready
     lds_u32 *const cns_addr = lane == 0 ? consumed_l + wv : scratch;   // ring wv consumed
+    lds_u32 *const in_base = in_l + lane * 4;
+    lds_u32 *const rd_base = ring_l + (wv - 1) * NS * SLOT + lane;  // ring wv (wv >= 1)
+    lds_u32 *const wr_base = ring_l + wv * NS * SLOT + lane;        // ring wv+1 (wv < P-1)
 
-    Pipe<KX, 1> p;
-    pipe_init(p);
+    PairState<1> st[KW];
+#pragma unroll
+    for (int g = 0; g < KW; ++g) { st[g].a0[0] = 0; st[g].a1[0] = 0; st[g].b0[0] = 0; st[g].b1[0] = 0; st[g].cb[0] = 0; }
     uint32_t alive = 0;
     const uint32_t nrows = (uint32_t)(s1 - s0);
-    // last wave: output row y = out_row(t) stored at voffset st_off + (y - s0) * pitch of ONE
-    // buffer spanning the strip's rows (the host keeps rows x pitch < 2^31): rows before s0
-    // (negative offsets, as unsigned >= 2^32 - 2K * pitch), from s1 on, and a halo lane's 2^31
-    // fall outside it, so no per-row descriptor or branch (as in band_pipe_kernel)
+    // last wave: output row y stored at voffset st_off + (y - s0) * pitch of ONE buffer spanning
+    // the strip's rows (the host keeps rows x pitch < 2^31): rows before s0 (negative offsets, as
+    // unsigned >= 2^32 - 2K * pitch), from s1 on, and a halo lane's 2^31 fall outside it
     const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
         dst_b + (int64_t)s0 * pitch, (short)0, (int)(nrows * (uint32_t)pitch), 0x00020000);
-    int rrel = out_row(0) - s0;  // output row - s0 of stream position 3b + S (wave-uniform)
+    int rrel = dir >= 0 ? -2 * K : s1e - 1 + 2 * K - s0;  // output row - s0 of the next row (wave-uniform)
     const int rstep = dir >= 0 ? 1 : -1;
     uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch;
     const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch;
-    // ready flags count published blocks; the first wave ends the stream with FINAL | blocks,
-    // which every wave passes on after its last block (a paired pipeline learns its block count
-    // only when a claim fails)
-    constexpr int FINAL = 1 << 30;
-    const int nclaim = (s1e - s0 + 4 * K) / 3;  // blocks of the pair
-    const int chunk = a.sm.chunk;
-    auto run = [&](auto role_c) -> bool {
-        constexpr int ROLE = decltype(role_c)::value;  // 0 first, 1 middle, 2 last
-        constexpr int NSTG = ROLE == 0 ? KF : (ROLE == 2 ? KL : KM);
-        int seen_ready = 0, seen_free = 0;
-        int nb = nblk;        // role 0: blocks granted so far
-        uint32_t next = 0;    // role 0, paired: blocks claimed before the pending claim
-        if constexpr (ROLE == 0) {
-            if (dir) {
-                // lane 0 claims (see band_pipe_kernel); a claim's return is waited for where it
-                // is used
-                uint32_t c0 = 0;
-                if (lane == 0) c0 = atomicAdd(ctr, (uint32_t)chunk);
-                c0 = __builtin_amdgcn_readfirstlane(c0);
-                nb = c0 >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c0);
-                if (nb == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);  // prefetched claim
-            }
+    // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit takes its shift
+    // mod 32), unpack through the LUT, store, count
+    auto emit = [&](uint32_t w) {
+        const uint32_t nxw = from_upper_lane(w);
+        const uint32_t o = K % 32 ? __builtin_amdgcn_alignbit(nxw, w, K % 32) : nxw;
+        uint2 e[4];
 #pragma unroll
-            for (int i = 0; i < NSI - 1; ++i) stage_in(i, in_ring[i]);
+        for (int q = 0; q < 4; ++q) e[q] = lut[(o >> (8 * q)) & 0xFF];
+        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[0].x, e[0].y, e[1].x, e[1].y}, strip_rs, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[2].x, e[2].y, e[3].x, e[3].y}, strip_rs, voff + 16u, 0, 0);
+        if constexpr (COUNT) {
+            const uint32_t c = __popc(o) + alive;
+            alive = (uint32_t)rrel < nrows ? c : alive;
         }
-        // Readers (waves 1 .. P-1): block b+1's rows are read at the end of block b (spinning
-        // there for its flag if needed) and waited for at the top of block b+1; a middle wave
-        // publishes "blocks < b ready" right after that wait, which also covers its writes of
-        // block b-1 (a wave's LDS operations complete in order), so no wave waits for its own
-        // writes.  The first wave publishes after its block's compute (its writes of the
-        // previous block are long done by then).
-        uint32_t nx[3] = {0, 0, 0};
-        bool more = true;
-        if constexpr (ROLE != 0) {
-            if (seen_ready < 1) {
-                seen_ready = spin_until_ge<true>(ready_l + wv, 1);
+        voff += vstep;
+        rrel += rstep;
+    };
+    constexpr int FINAL = 1 << 30;  // ready flag = FINAL + blocks: the stream has ended
+    uint32_t pending = 0;  // the loader's claim in flight (paired)
+    if (wv == 0 && dir && lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
+    // block 0's rows read to completion here (the compiler copies loop-carried registers on loop
+    // entry, which must not happen while a read is in flight).  A reader's next block (RPB words)
+    // is read at the end of a block; the loader reads its block's 2 RPB 16-byte halves at the
+    // block's start (32 VGPRs held across the compute would spill at 6 waves per SIMD).
+    v4u32 nb[2 * RPB];  // loader
+    uint32_t nw[RPB];   // readers
+    int seen_ready = 0, seen_free = 0;
+    auto read_in = [&](auto off_c) {  // the loader's reads of one input slot
+        constexpr int OFF = decltype(off_c)::value;
+        static_assert(RPB == 4, "eight half-row reads");
+        nb[0] = lds_rd128_issue_o<OFF>(in_base);
+        nb[1] = lds_rd128_issue_o<OFF + 1024>(in_base);
+        nb[2] = lds_rd128_issue_o<OFF + 2048>(in_base);
+        nb[3] = lds_rd128_issue_o<OFF + 3072>(in_base);
+        nb[4] = lds_rd128_issue_o<OFF + 4096>(in_base);
+        nb[5] = lds_rd128_issue_o<OFF + 5120>(in_base);
+        nb[6] = lds_rd128_issue_o<OFF + 6144>(in_base);
+        nb[7] = lds_rd128_issue_o<OFF + 7168>(in_base);
+    };
+    auto read_ring = [&](auto off_c) {  // a reader's reads of one ring slot
+        constexpr int OFF = decltype(off_c)::value;
+        static_assert(RPB == 4, "four row reads");
+        nw[0] = lds_rd32_issue_o<OFF>(rd_base);
+        nw[1] = lds_rd32_issue_o<OFF + 256>(rd_base);
+        nw[2] = lds_rd32_issue_o<OFF + 512>(rd_base);
+        nw[3] = lds_rd32_issue_o<OFF + 768>(rd_base);
+    };
+    auto settle_in = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2 * RPB; ++h) lds_settle<0>(nb[h]);
+    };
+    if (wv == 0) {
+        stage_in(0, in_ring[0]);
+        stage_in(1, in_ring[1]);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RPB) : "memory");  // block 0 landed (the claim before it too)
+#pragma unroll
+        for (int S = 0; S < RPB; ++S) nw[S] = 0;
+    } else {
+        seen_ready = spin_until_ge<true>(ready_l + wv, 1);
+        if (seen_ready < 0) {
+            raise_error(a.err, GOLK_ERR_SPIN);
+            return;
+        }
+        read_ring(std::integral_constant<int, 0>());
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nw[0]), "+v"(nw[1]), "+v"(nw[2]), "+v"(nw[3])::"memory");
+    }
+    bool more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
+    // Fill blocks (band_pipe_kernel's rule): a wave whose first stage is g0 = KW * wv passes the
+    // blocks that end before step 2 g0 (RPB b + RPB <= 2 g0) on without the rule -- a uniform
+    // branch per block here (the byte pipeline has registers to spare; a loop of its own per role
+    // doubled the role's code)
+    const int nskip = 2 * KW * wv / RPB;
+    auto step = [&](int b, auto u_c, auto role_c, auto dyn_c) -> bool {
+        constexpr int US = decltype(u_c)::value;
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool DYN = decltype(dyn_c)::value;
+        constexpr bool LAST = ROLE == 2;
+        constexpr int NXT = (US + 1) % NS;
+        uint32_t r[RPB];
+        // block b's rows, the youngest LDS operations of this wave: once they are in, so are
+        // block b-1's row writes, and both flags can go out at once
+        if constexpr (ROLE == 0) {
+            read_in(std::integral_constant<int, US % NSI * ISB>());
+            settle_in();
+#pragma unroll
+            for (int S = 0; S < RPB; ++S)
+                r[S] = pack32_ff(uint4{nb[2 * S].x, nb[2 * S].y, nb[2 * S].z, nb[2 * S].w},
+                                 uint4{nb[2 * S + 1].x, nb[2 * S + 1].y, nb[2 * S + 1].z, nb[2 * S + 1].w});
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nw[0]), "+v"(nw[1]), "+v"(nw[2]), "+v"(nw[3])::"memory");
+#pragma unroll
+            for (int S = 0; S < RPB; ++S) r[S] = nw[S];
+            lds_flag_wr(cns_addr, b + 1);  // block b's slot is free
+        }
+        if constexpr (!LAST) lds_flag_wr(rdy_addr, b);  // blocks < b are in ring wv+1
+        if (ROLE == 0 || b >= nskip) {
+            // stage step w: the first pair at stage w, the second at stage w-1 (each stage takes
+            // its pairs in stream order)
+#pragma unroll
+            for (int w = 0; w <= KW; ++w) {
+                if (w < KW) spstage(st[w], r[0], r[1]);
+                if (w >= 1) spstage(st[w - 1], r[2], r[3]);
+            }
+        }
+        if constexpr (LAST) {
+#pragma unroll
+            for (int S = 0; S < RPB; ++S) emit(r[S]);
+        } else {
+            if (seen_free < b + 1 - NS) {  // slot b % NS: block b - NS consumed
+                seen_free = spin_until_ge<true>(consumed_l + wv + 1, b + 1 - NS);
+                if (seen_free < 0) return false;
+            }
+            static_assert(RPB == 4, "four row writes");
+            lds_wr32_o<US * SB>(wr_base, r[0]);
+            lds_wr32_o<US * SB + RB>(wr_base, r[1]);
+            lds_wr32_o<US * SB + 2 * RB>(wr_base, r[2]);
+            lds_wr32_o<US * SB + 3 * RB>(wr_base, r[3]);
+        }
+        // block b+1's rows: read now, waited for at the next block's start
+        if constexpr (ROLE == 0) {
+            stage_in(b + 2, in_ring[(US + 2) % NSI]);  // refills block b+2-NSI's slot (clamped past the end)
+            // block b+1 landed, b+2 in flight (2 RPB loads; and, paired, at US 1 the claim issued at US 0)
+            if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RPB + 1) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RPB) : "memory");
+            if constexpr (DYN && US == 0) {
+                if (lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
+            }
+        } else {
+            // the next block exists unless the writer's flag says the stream ended before it
+            if (seen_ready < b + 2) {
+                seen_ready = spin_until_ge<true>(ready_l + wv, b + 2);
                 if (seen_ready < 0) return false;
             }
-            more = !(seen_ready >= FINAL && seen_ready - FINAL == 0);
-            if (more) lds_rd32x3_issue(slot_row(wv, 0, 0), nx);
+            more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
+            read_ring(std::integral_constant<int, NXT * SB>());
         }
+        return true;
+    };
+    auto grant = [&](uint32_t c) { return c >= (uint32_t)nclaim ? 0 : NS; };
+
+    auto trip = [&](int b, auto role_c, auto dyn_c) -> bool {
+        bool ok = true;
+        static_for<NS>([&](auto u_c) {
+            if (ok) ok = step(b + decltype(u_c)::value, u_c, role_c, dyn_c);
+        });
+        return ok;
+    };
+    auto run = [&](auto role_c, auto dyn_c) -> bool {
+        constexpr int ROLE = decltype(role_c)::value;
+        constexpr bool DYN = decltype(dyn_c)::value;
+        int nb = DYN ? 0 : (nblk + NS - 1) / NS * NS;
         int b = 0;
-        int wsl = 0, rsl = 1 % NS, isl = 0;  // b % NS, (b + 1) % NS, b % NSI
-        const int g0 = ROLE == 0 ? 0 : (ROLE == 2 ? K - KL : KF + (wv - 1) * KM);  // first stage of this wave
-        const int skip_b = (2 * g0) / 3;  // blocks 0 .. skip_b-1 end before step 2 g0
-        for (;; ++b, wsl = next_slot(wsl, NS), rsl = next_slot(rsl, NS), isl = next_slot(isl, NSI)) {
-            uint32_t w3[3];
+        for (;; b += NS) {
             if constexpr (ROLE == 0) {
-                if (b >= nb) {
-                    if (!dir || nb % chunk != 0 || nb == 0) break;
-                    const uint32_t c = __builtin_amdgcn_readfirstlane(next);
-                    const int g = c >= (uint32_t)nclaim ? 0 : min(chunk, nclaim - (int)c);
-                    if (g == 0) break;
-                    nb += g;
-                    if (g == chunk && lane == 0) next = atomicAdd(ctr, (uint32_t)chunk);
-                }
-                // block b landed (blocks b+1 .. b+NSI-2 may still be in flight: 6 loads each)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSI - 2) * 6) : "memory");
-                v4u32 raw[6];
-                lds_rd_block6(in_l + isl * (3 * 2 * 256) + lane * 4, raw);
-#pragma unroll
-                for (int S = 0; S < 3; ++S)
-                    w3[S] = pack32_ff(uint4{raw[2 * S].x, raw[2 * S].y, raw[2 * S].z, raw[2 * S].w},
-                                      uint4{raw[2 * S + 1].x, raw[2 * S + 1].y, raw[2 * S + 1].z, raw[2 * S + 1].w});
-                // refill block b-1's slot (read to completion in the previous trip; clamped past the end)
-                stage_in(b + NSI - 1, in_ring[isl == 0 ? NSI - 1 : isl - 1]);
+                if constexpr (DYN) nb += grant(__builtin_amdgcn_readfirstlane(pending));
+                if (b >= nb) break;
             } else {
                 if (!more) break;
-                lds_wait3(nx);  // block b's rows (and every older LDS operation of this wave)
-                w3[0] = nx[0]; w3[1] = nx[1]; w3[2] = nx[2];
-                lds_flag_wr(cns_addr, b + 1);
-                if constexpr (ROLE == 1) lds_flag_wr(rdy_addr, b);  // blocks < b: written and complete
             }
-            // Fill rows: stage g's input is valid from stream step 2g on (each stage needs the two
-            // rows before), and only its outputs from step 2g + 2 on are ever used, so a wave whose
-            // first stage is g0 skips the blocks that end before step 2 g0 (their rows pass on as
-            // they are; its pipe state is stale until step 2 g0, where nothing needs it yet).
-            if (b >= skip_b) sstage_waves3<KX, NSTG>(p, w3, std::make_integer_sequence<int, NSTG + 2>());
-            if constexpr (ROLE == 2) {
-                // undo the K-bit frame shift (K = 32: exactly the next lane's word; alignbit takes
-                // its shift mod 32), unpack row by row through the LUT (all 12 reads ahead of the
-                // stores measured 0.9 % slower)
-                uint32_t o[3];
-                uint2 e[3][4];
-#pragma unroll
-                for (int S = 0; S < 3; ++S) {
-                    const uint32_t nxw = from_upper_lane(w3[S]);
-                    o[S] = K % 32 ? __builtin_amdgcn_alignbit(nxw, w3[S], K % 32) : nxw;
-                }
-#pragma unroll
-                for (int S = 0; S < 3; ++S) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) e[S][q] = lut[(o[S] >> (8 * q)) & 0xFF];
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[S][0].x, e[S][0].y, e[S][1].x, e[S][1].y}, strip_rs, voff, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[S][2].x, e[S][2].y, e[S][3].x, e[S][3].y}, strip_rs, voff + 16u, 0, 0);
-                    if constexpr (COUNT)
-                        alive += bitop3<0x80>((uint32_t)__popc(o[S]), st_mask, (uint32_t)rrel < nrows ? 0xFFFFFFFFu : 0u);
-                    voff += vstep;
-                    rrel += rstep;
-                }
-            } else {
-                if constexpr (ROLE == 0) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // block b-1's writes
-                    lds_flag_wr(rdy_addr, b);
-                }
-                if (seen_free < b + 1 - NS) {
-                    seen_free = spin_until_ge<true>(consumed_l + wv + 1, b + 1 - NS);
-                    if (seen_free < 0) return false;
-                }
-#pragma unroll
-                for (int S = 0; S < 3; ++S) lds_wr32(slot_row(wv + 1, wsl, S), (int)w3[S]);
-            }
-            if constexpr (ROLE != 0) {
-                if (seen_ready < b + 2) {
-                    seen_ready = spin_until_ge<true>(ready_l + wv, b + 2);
-                    if (seen_ready < 0) return false;
-                }
-                more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
-                if (more) lds_rd32x3_issue(slot_row(wv, rsl, 0), nx);
-            }
+            if (!trip(b, role_c, dyn_c)) return false;
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last block's reads of the next slot
         if constexpr (ROLE != 2) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_flag_wr(rdy_addr, FINAL + b);
         }
-        if constexpr (ROLE == 0) {
-            if (dir && lane == 0) {
-                // this pipeline's claims are over (none in flight): the second of the pair to get
-                // here zeroes the counters for the next launch
-                if (atomicAdd(ctr + 1, 1u) == 1u) {
-                    atomicExch(ctr, 0u);
-                    atomicExch(ctr + 1, 0u);
-                }
+        if constexpr (ROLE == 0 && DYN) {
+            if (lane == 0 && atomicAdd(ctr + 1, 1u) == 1u) {  // both loaders' claims are over
+                atomicExch(ctr, 0u);
+                atomicExch(ctr + 1, 0u);
             }
         }
         return true;
     };
+    // (paired or not changes only the loader's loop: the readers' loops are one instantiation,
+    // which halves their code -- the I-cache holds 64 KiB for two CUs)
+    auto run_role = [&](auto role_c) -> bool {
+        if constexpr (decltype(role_c)::value != 0) return run(role_c, std::false_type());
+        else return dir ? run(role_c, std::true_type()) : run(role_c, std::false_type());
+    };
     bool ok;
-    if (wv == 0) ok = run(std::integral_constant<int, 0>());
-    else if (wv == P - 1) ok = run(std::integral_constant<int, 2>());
-    else ok = run(std::integral_constant<int, 1>());
+    if (wv == 0) ok = run_role(std::integral_constant<int, 0>());
+    else if (wv == P - 1) ok = run_role(std::integral_constant<int, 2>());
+    else ok = run_role(std::integral_constant<int, 1>());
     if (wv == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // input blocks staged past the end
     if (!ok) raise_error(a.err, GOLK_ERR_SPIN);
+    alive &= st_mask;  // halo lanes' rows are not this group's
     if (COUNT && wv == P - 1) slot_add(a.slots, alive);
 }
 
-#ifndef GOL_BYTES_PIPE_STAGES
-#define GOL_BYTES_PIPE_STAGES 4, 4, 4
+#ifndef GOL_BYTES_PIPE_KW
+#define GOL_BYTES_PIPE_KW 4
 #define GOL_BYTES_PIPE_P 8
 #endif
-#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_STAGES, GOL_BYTES_PIPE_P, count>)
+#define BYTES_PIPE(count) (bytes_pipe_kernel<GOL_BYTES_PIPE_KW, GOL_BYTES_PIPE_P, count>)
+
+
 
 #ifdef GOL_TU_BYTES_PIPE
 }  // namespace golk
@@ -2650,7 +2708,7 @@ hipError_t golk_bytes_blocked(const uint8_t *top, const uint8_t *mid, const uint
         const int64_t max_rows = std::max<int64_t>(1, ((int64_t(1) << 31) - 1) / pitch - 1);
         if (strip <= 0 && cus > 0 &&
             rank_split(rows, a.ngroups, cus, (int)std::min<int64_t>(GOL_BYTES_PER_CU, slots / cus), BYTES_PIPE_RANK_W,
-                       2 * k, 1024, a.sm, claims != nullptr, claims, 4) && a.sm.period <= max_rows) {
+                       2 * k, 1024, a.sm, claims != nullptr, claims, GOL_BYTES_NS) && a.sm.period <= max_rows) {
             nwg = (int64_t)cus * a.sm.per_cu;
         } else {
             a.sm = StripMap{};

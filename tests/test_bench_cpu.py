@@ -33,7 +33,7 @@ def test_self_launch_two_ranks_dry_run():
     assert rs["launch_ms"] == {"max": 0.5, "min": 0.25}
     assert rs["exchange_ms"] == {"max": 0.02, "min": 0.01}
     assert rs["wall_ms"] == {"max": 2.0, "min": 1.0}
-    assert rs["nranks_seen"] == [2, 2] and rs["exchanges_per_rank"] == [4, 4]
+    assert rs["nranks_seen"] == [2, 2] and rs["exchanges_per_rank"] == [20, 20]  # (the warmup's: weak's default 20)
     assert rs["transports"] == ["dry-run"] and "basis" in rs
 
 
