@@ -16,7 +16,8 @@ its halo exchange and the fused AliveCellsCount):
   strong262k  262144 x 262144 bit-packed torus sharded over the N ranks (config 4; total work
            fixed as N grows, "scaling": "strong").
   bit64k   65536 x 65536 bit-packed torus on one GPU (config 3); replicas for N > 1.
-  byte16k  16384 x 16384 byte-per-cell torus, k = 32 turns per launch (config 2); replicas for N > 1.
+  byte16k  16384 x 16384 byte-per-cell torus (config 2): the engine's byte board (GOL_LAYOUT_BYTES),
+           k = 32 turns per launch of the byte pipeline; replicas for N > 1.
 
 Inputs are synthetic (splitmix64 Bernoulli(1/2) cells, generated on the GPU) and resident in
 HBM before timing.  Rank 0 prints one JSON line.  (GOL_BENCH_STACKS_AFTER_S=N: every thread's
@@ -435,73 +436,39 @@ def settle_steps(args, run_n, cell_updates_per_step, nominal_rate):
 
 
 def run_bytes(args, ranks):
-    """Config 2: 16384 x 16384 byte-per-cell torus.  The board stays one byte per cell in HBM; each
-    launch runs k turns (gol_dev_bytes_step_k: 0/255 bytes packed to bits in registers); k = 1
-    is the exact one-turn byte kernel (gol_dev_bytes_step)."""
-    import ctypes
-
-    import torch
-    from golhip._lib import check, lib
-    from golhip.sharded import HipKernels
-    torch.cuda.set_device(ranks.local)
+    """Config 2: 16384 x 16384 byte-per-cell torus, stepped by the engine on its byte board
+    (GOL_LAYOUT_BYTES: the board stays one byte per cell in HBM, as the reference's worker holds
+    it; each launch runs k = 32 turns of the byte pipeline, 0/255 bytes packed to bits in
+    registers, with the alive count fused).  The same cells as the bit workloads' load_random(1)."""
+    import golhip
     H = W = 16384
-    Wd = W // 32
-    bits = torch.empty((H, Wd), dtype=torch.int32, device="cuda")
-    kern = HipKernels()
-    kern.Wd = Wd
-    kern.random_fill(bits, 0, W, 1)
-    a = kern.unpack(bits, W)
-    b = torch.empty_like(a)
-    del bits
-    stream = torch.cuda.current_stream().cuda_stream
-    k = max(kk for kk in (32, 16, 8, 4, 2, 1) if kk <= args.k)
-    # one zeroed slot array per counted step (the kernel's fused count lands in its own array: no
-    # memset between steps); the per-step sums are taken once, inside the timed region
-    nslots = 256 * 8
-    slots = torch.zeros((max(args.warmup, args.steps), nslots), dtype=torch.int64, device="cuda")
-    cur = [a, b]
-
-    def step(i):
-        src, dst = cur
-        if k == 1:
-            check(lib().gol_dev_bytes_step(src.data_ptr(), H, W, W, 0, H, dst.data_ptr(), W, stream))
-        else:
-            check(lib().gol_dev_bytes_step_k(src[H - k:].data_ptr(), src.data_ptr(), src.data_ptr(), dst.data_ptr(),
-                                             H, W, W, 0, H, k, args.strip, slots[i].data_ptr(), stream))
-        cur.reverse()
-
-    def steps_n(n):
-        for i in range(n):
-            step(i % slots.shape[0])
-    settle = settle_steps(args, steps_n, float(H) * W * k, SETTLE_RATE_BYTES)
-    for i in range(args.warmup):
-        step(i)
-    # (the count's reduction below is loaded and run once here: a first use inside the timed region
-    # would load its code object there)
-    _ = slots[:1].view(1, 256, 8)[:, :, 0].sum(dim=1)
-    slots.zero_()
+    e = golhip.Engine(H, W, device=ranks.local, turns_per_launch=args.k, strip_rows=args.strip, layout="bytes")
+    info = e.info()
+    assert info["layout"] == "bytes", info
+    k = info["turns_per_launch"]
+    e.load_random(1)
+    settle = settle_steps(args, lambda n: e.step_counted(n * k, k), float(H) * W * k, SETTLE_RATE_BYTES)
+    if args.warmup:
+        e.step_counted(args.warmup * k, k)
     ranks.barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e.set_timing(True)
     t0 = time.perf_counter()
-    ev0.record()
-    for i in range(args.steps):
-        step(i)
-    ev1.record()
-    counts = slots[:args.steps].view(args.steps, 256, 8)[:, :, 0].sum(dim=1) if k > 1 else None
-    torch.cuda.synchronize()
+    counts = e.step_counted(args.steps * k, k)  # one launch (+ fused count) per step
     dt = time.perf_counter() - t0
     ranks.barrier()
-    flags = ctypes.c_uint32()
-    check(lib().gol_dev_error(ranks.local, ctypes.byref(flags)))
+    t = e.timing()
+    e.set_timing(False)
+    e.close()
     dt = ranks.max(dt)
     value = H * W * ranks.world * k * args.steps / dt
-    kms = ev0.elapsed_time(ev1) / args.steps  # HIP events around the timed launches, per launch
-    alive = int(counts[-1].item()) if counts is not None else None
+    alive = int(counts[-1]) if len(counts) else None
+    if ranks.world > 1:
+        alive = int(ranks.sum(alive))  # independent replicas
     pmc, note = load_pmc(f"byte16k:{H}x{W}:k{k}:bytes")
-    roof = roofline("bytes", kms, float(H * W * k), pmc, note)
-    cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k,
+    roof = roofline("bytes", t["mean_ms"], t["mean_cell_updates"], pmc, note)
+    cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k, "layout": "bytes",
            "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "1gpu",
-           "alive_count_every_step": k > 1, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
+           "alive_count_every_step": True, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
            "settle_steps": settle}
     return value, dt, cfg, roof, "u8 (byte per cell)"
 

@@ -174,7 +174,10 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
         return gol_set_error(GOL_EINVAL, "bad board size %lldx%lld", (long long)W, (long long)H);
     e->H = H;
     e->W = W;
-    e->bit_capable = (W % 64) == 0;
+    const int layout = cfg ? cfg->layout : GOL_LAYOUT_AUTO;
+    if (layout < GOL_LAYOUT_AUTO || layout > GOL_LAYOUT_BYTES)
+        return gol_set_error(GOL_EINVAL, "layout must be GOL_LAYOUT_AUTO, _STANDARD, _BAND or _BYTES");
+    e->bit_capable = (W % 64) == 0 && layout != GOL_LAYOUT_BYTES;
     e->mode = e->bit_capable ? GOL_MODE_BITS : GOL_MODE_BYTES;
     e->Wd = W / 32;
     e->pitch = (e->Wd + 3) / 4 * 4;
@@ -187,12 +190,11 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
     while (e->dw > 1 && (e->Wd % e->dw) != 0) e->dw >>= 1;
     e->band_dw = req == 64 ? 2 : (req == 128 ? 4 : GOL_BAND_DEFAULT_DW);
     e->strip = cfg ? cfg->strip_rows : 0;
-    const int layout = cfg ? cfg->layout : GOL_LAYOUT_AUTO;
-    if (layout != GOL_LAYOUT_AUTO && layout != GOL_LAYOUT_STANDARD && layout != GOL_LAYOUT_BAND)
-        return gol_set_error(GOL_EINVAL, "layout must be GOL_LAYOUT_AUTO, _STANDARD or _BAND");
     if (layout == GOL_LAYOUT_BAND && W % 1024 != 0) return gol_set_error(GOL_EINVAL, "the band layout needs W %% 1024 == 0");
-    e->band_capable = layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
-    if (e->k == 0) e->k = (e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K;
+    e->band_capable = e->bit_capable && layout != GOL_LAYOUT_STANDARD && W % 1024 == 0;
+    if (e->k == 0)
+        e->k = !e->bit_capable ? GOL_DEFAULT_BYTES_K
+                               : ((e->band_capable && e->band_dw == 4) ? GOL_DEFAULT_BAND_K : GOL_DEFAULT_K);
     e->step_flags = cfg ? (cfg->flags & (GOL_STEP_SERIAL | GOL_STEP_EDGE_FIRST | GOL_STEP_OVERLAP)) : 0;
     return GOL_OK;
 }
@@ -201,7 +203,7 @@ static int engine_setup(gol_engine *e, int64_t H, int64_t W, const gol_config *c
 static int engine_shards(gol_engine *e, const std::vector<int> &devices)
 {
     if (e->nranks > 1 && !e->bit_capable)
-        return gol_set_error(GOL_EINVAL, "a sharded board needs W %% 64 == 0 (W = %lld)", (long long)e->W);
+        return gol_set_error(GOL_EINVAL, "a sharded board needs a bit board: W %% 64 == 0 (W = %lld), layout not BYTES", (long long)e->W);
     if (e->H < e->nranks)
         return gol_set_error(GOL_EINVAL, "%d shards cannot split %lld rows", e->nranks, (long long)e->H);
     e->min_rows = e->H / e->nranks;  // broker.go:172-206: the smallest shard
@@ -944,7 +946,7 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
             n -= 1;
             continue;
         }
-        if (e->mode == GOL_MODE_BYTES) {  // W % 64 != 0: one shard, the byte board
+        if (e->mode == GOL_MODE_BYTES) {  // W % 64 != 0 or GOL_LAYOUT_BYTES: one shard, the byte board
             gol_shard &s = e->sh[0];
             RCCHK(set_dev(s.device));
             const uint8_t *mid = s.bytes[e->bcur];
@@ -956,6 +958,10 @@ static int advance(gol_engine *e, int64_t n, int64_t ci)
                 HIPCHK(golk_bytes_blocked(mid + (e->H - k) * e->bstride, mid, mid, s.bytes[1 - e->bcur], e->H, e->W,
                                           e->bstride, 0, e->H, k, e->strip, last ? batch_slots(s, ci) : nullptr, s.err,
                                           s.stream));
+                if (timing_open(e)) {
+                    e->tcall_cells[0] += (double)e->H * (double)e->W * k;
+                    e->tcall_steps += 1;
+                }
                 e->bcur = 1 - e->bcur;
                 e->turn += k;
                 n -= k;
@@ -1087,7 +1093,7 @@ extern "C" int gol_engine_alive_count(gol_engine *e, uint64_t *count)
 extern "C" int gol_engine_hash(gol_engine *e, uint64_t *hash)
 {
     if (!e || !hash) return gol_set_error(GOL_EINVAL, "bad arguments");
-    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "hash needs W %% 64 == 0");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "hash needs a bit board (W %% 64 == 0, layout not BYTES)");
     RCCHK(ensure_standard(e));
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
@@ -1205,8 +1211,23 @@ extern "C" int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_
 extern "C" int gol_engine_load_random(gol_engine *e, uint64_t seed)
 {
     if (!e) return gol_set_error(GOL_EINVAL, "engine is NULL");
-    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "random boards need W %% 64 == 0");
+    if (e->W % 64 != 0) return gol_set_error(GOL_EINVAL, "random boards need W %% 64 == 0");
     RCCHK(reset_board_state(e));
+    if (!e->bit_capable) {  // GOL_LAYOUT_BYTES: the same cells as 0/255 bytes (fill bits, then unpack)
+        gol_shard &s = e->sh[0];
+        RCCHK(set_dev(s.device));
+        uint32_t *bits = nullptr;
+        HIPCHK(hipMalloc((void **)&bits, e->H * e->pitch * sizeof(uint32_t)));
+        hipError_t err = golk_random_fill(bits, e->H, 0, e->W, e->pitch, seed, s.stream);
+        if (err == hipSuccess) err = golk_unpack(bits, e->H, e->W, e->pitch, s.bytes[0], e->bstride, s.stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(s.stream);
+        const hipError_t ferr = hipFree(bits);
+        HIPCHK(err);
+        HIPCHK(ferr);
+        e->bytes_binary = true;
+        e->mode = GOL_MODE_BYTES;
+        return GOL_OK;
+    }
     for (auto &s : e->sh) {
         RCCHK(set_dev(s.device));
         free_exact_bytes(s);
@@ -1638,7 +1659,7 @@ static int rows_check(gol_engine *e, int64_t y0, int64_t y1, const void *p, int6
 {
     if (!e || !p || y0 < 0 || y1 > e->H || y0 > y1 || stride < e->W / 64)
         return gol_set_error(GOL_EINVAL, "bad word-row arguments");
-    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "bit-packed rows need W %% 64 == 0");
+    if (!e->bit_capable) return gol_set_error(GOL_EINVAL, "bit-packed rows need a bit board (W %% 64 == 0, layout not BYTES)");
     if (y0 < e->sh.front().y0 || y1 > e->sh.back().y1)
         return gol_set_error(GOL_EINVAL, "rows [%lld, %lld) are not held by this process", (long long)y0, (long long)y1);
     return GOL_OK;
@@ -1690,7 +1711,8 @@ extern "C" int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lan
     const bool bits = e->mode == GOL_MODE_BITS;
     const bool band = bits && e->band_capable;
     const int dw = band ? e->band_dw : e->dw;
-    const int kk = pick_k(e->k, e->k, e->min_rows, dw, band);
+    const bool pipe32 = e->mode == GOL_MODE_BYTES && e->k >= 32 && e->H >= 32 && e->W % 32 == 0;  // (advance)
+    const int kk = pipe32 ? 32 : pick_k(e->k, e->k, e->min_rows, dw, band);
     if (k) *k = kk;
     if (cells_per_lane) *cells_per_lane = 32 * dw;
     if (strip_rows) {

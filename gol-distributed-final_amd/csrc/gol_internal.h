@@ -16,6 +16,7 @@ class gol_ipc;
 // in DESIGN.md; overridable per engine through gol_config).
 #define GOL_DEFAULT_K 8        // standard layout
 #define GOL_DEFAULT_BAND_K 12  // band layout, 4 words per lane: the split pipeline
+#define GOL_DEFAULT_BYTES_K 32 // byte board: the byte pipeline (0/255 boards with W % 32 == 0)
 #define GOL_DEFAULT_DW 2       // standard layout: 64 cells per lane
 
 // A step whose launch runs more rounds of workgroups than this overlaps its edge launches with
@@ -70,7 +71,7 @@ struct gol_shard {
 
 enum gol_mode {
     GOL_MODE_BITS,   // bit board (W % 64 == 0)
-    GOL_MODE_BYTES,  // byte board: W % 64 != 0 (one shard)
+    GOL_MODE_BYTES,  // byte board: W % 64 != 0 or GOL_LAYOUT_BYTES (one shard)
     GOL_MODE_EXACT   // bit-capable board loaded with bytes other than 0/255: turn 1 is exact
 };
 
@@ -97,7 +98,7 @@ struct gol_engine {
     std::vector<int> ipc_peers;  // global ranks this rank pulls its halo from (itself excluded)
     uint32_t xn = 0;           // halo exchanges issued (IPC sequence numbers; equal on every rank)
     int64_t min_rows = 0;    // rows of the smallest shard (the broker split: H / nranks)
-    bool bit_capable = false;  // W % 64 == 0
+    bool bit_capable = false;  // W % 64 == 0 and not GOL_LAYOUT_BYTES
     bool band_capable = false; // step the bit board in the band layout
     bool band = false;         // bits[cur] currently hold the band layout
     gol_mode mode = GOL_MODE_BITS;

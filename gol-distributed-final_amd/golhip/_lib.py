@@ -26,8 +26,9 @@ GOL_RCCL_ID_BYTES = 128
 GOL_TIMING_EXCHANGE = 2
 GOL_IPC_ID_BYTES = 128
 GOL_IPC_MAX_RANKS = 16
-GOL_LAYOUT_AUTO, GOL_LAYOUT_STANDARD, GOL_LAYOUT_BAND = 0, 1, 2
-LAYOUTS = {"auto": GOL_LAYOUT_AUTO, "standard": GOL_LAYOUT_STANDARD, "band": GOL_LAYOUT_BAND}
+GOL_LAYOUT_AUTO, GOL_LAYOUT_STANDARD, GOL_LAYOUT_BAND, GOL_LAYOUT_BYTES = 0, 1, 2, 3
+LAYOUTS = {"auto": GOL_LAYOUT_AUTO, "standard": GOL_LAYOUT_STANDARD, "band": GOL_LAYOUT_BAND,
+           "bytes": GOL_LAYOUT_BYTES}
 GOL_TRANSPORT_AUTO, GOL_TRANSPORT_LOOPBACK, GOL_TRANSPORT_RCCL, GOL_TRANSPORT_LOCAL, GOL_TRANSPORT_IPC = 0, 1, 2, 3, 4
 TRANSPORTS = {"auto": GOL_TRANSPORT_AUTO, "loopback": GOL_TRANSPORT_LOOPBACK, "rccl": GOL_TRANSPORT_RCCL,
               "ipc": GOL_TRANSPORT_IPC}

@@ -210,7 +210,7 @@ class Engine:
         self._check(self._L.gol_engine_info(self._h, ctypes.byref(k), ctypes.byref(cpl), ctypes.byref(strip),
                                     ctypes.byref(bm)))
         return {"turns_per_launch": k.value, "cells_per_lane": cpl.value, "strip_rows": strip.value,
-                "bit_mode": bool(bm.value), "layout": {0: None, 1: "standard", 2: "band"}[bm.value]}
+                "bit_mode": bool(bm.value), "layout": {0: "bytes", 1: "standard", 2: "band"}[bm.value]}
 
     def topology(self) -> dict:
         s, n, r, t = (ctypes.c_int32() for _ in range(4))

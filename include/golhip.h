@@ -108,10 +108,15 @@ typedef struct gol_engine gol_engine;
  * 32s .. 32s+31.  BAND: word w holds, at bit b, cell b*(W/32) + w (32 column
  * bands), which makes a generation shift-free.  AUTO picks
  * BAND when W % 1024 == 0.  The layout is internal: every reader (store,
- * alive list, PGM, hash, device_bits) sees the standard layout. */
+ * alive list, PGM, hash, device_bits) sees the standard layout.  BYTES keeps
+ * the board as the reference's one byte per cell (a W % 64 != 0 board always
+ * does): one shard, 32 turns per launch on a 0/255 board with W % 32 == 0 (the
+ * byte pipeline), the exact byte kernel otherwise; the
+ * bit-board calls (load_words, store_words, device_bits, hash) are EINVAL. */
 #define GOL_LAYOUT_AUTO 0
 #define GOL_LAYOUT_STANDARD 1
 #define GOL_LAYOUT_BAND 2
+#define GOL_LAYOUT_BYTES 3
 /* Halo transport between shards. */
 #define GOL_TRANSPORT_AUTO 0     /* 1 shard: local torus wrap; shards on distinct GPUs: RCCL; else LOOPBACK */
 #define GOL_TRANSPORT_LOOPBACK 1 /* device copies between the shards of this process */
@@ -172,7 +177,8 @@ int gol_engine_load_bytes(gol_engine *e, const uint8_t *world, int64_t stride);
  * it. */
 int gol_engine_load_pgm(gol_engine *e, const char *path);
 /* Synthetic board: word(y, w) = splitmix64(seed ^ (y*W/64 + w)), Bernoulli(1/2)
- * per cell (W % 64 == 0 only).  Resets the turn counter. */
+ * per cell (W % 64 == 0 only; on a GOL_LAYOUT_BYTES board as 0/255 bytes).
+ * Resets the turn counter. */
 int gol_engine_load_random(gol_engine *e, uint64_t seed);
 /* Advance exactly `turns` turns (blocking).  Replaces the turn loop body of
  * broker.go:75-226. */

@@ -495,6 +495,44 @@ def test_byte_board_engine_counted_paired(golhip):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("shape", [(32, 64), (50, 128), (203, 2048), (1000, 4096), (4096, 32 * 97 * 2)])
+def test_bytes_layout_engine(golhip, shape):
+    """GOL_LAYOUT_BYTES keeps a W % 64 == 0 board as the reference's bytes (config 2's path through
+    the engine): load_random gives the bit boards' cells as 0/255, k = 32 launches take the byte
+    pipeline with the fused count, a short tail takes the blocked byte kernel; bit-board calls
+    are EINVAL."""
+    H, W = shape
+    words = O.random_words(7, 0, H, W // 64)
+    with golhip.Engine(H, W, device=0, layout="bytes") as e:
+        info = e.info()
+        assert info["layout"] == "bytes" and info["turns_per_launch"] == 32 and not info["bit_mode"]
+        e.load_random(7)
+        assert np.array_equal(e.store_bytes(), O.unpack(words))
+        counts = e.step_counted(64, 32)
+        e.step(5)
+        ref, rc = O.bits_run(words, 69, with_counts=True)
+        assert counts.tolist() == [rc[31], rc[63]]
+        assert np.array_equal(e.store_bytes(), O.unpack(ref))
+        assert e.alive_count() == rc[68] and e.turn == 69
+        with pytest.raises(golhip.GolError):
+            e.hash()
+
+
+def test_bytes_layout_timing_and_rank_refusal(golhip):
+    """The byte board's launches are timed like the bit board's (bench.py byte16k reads them), and
+    a byte board does not shard."""
+    H, W = 512, 1024
+    with golhip.Engine(H, W, device=0, layout="bytes") as e:
+        e.load_random(3)
+        e.set_timing(True)
+        e.step_counted(96, 32)
+        t = e.timing()
+        e.set_timing(False)
+        assert t["launches"] == 3 and t["mean_cell_updates"] == H * W * 32 and t["mean_ms"] > 0
+    with pytest.raises(golhip.GolError):
+        golhip.Engine(H, W, device=0, layout="bytes", shards=2, same_device=True)
+
+
 def test_band_paired_narrow_board(golhip):
     """One band column group (W = 2048) over 65536 rows: the one-round rank split gives every CU
     256 rows in two paired ranges of ~128 rows (4K = 48 rows of fill each); 25 turns (two k = 12
