@@ -46,8 +46,13 @@ func main() {
 	port := flag.String("port", "8040", "port to listen on") // broker.go:281
 	gpus := flag.Int("gpus", 1, "GPUs the board of a Run is row-sharded over")
 	k := flag.Int("k", 0, "turns per kernel launch (0 = library default)")
+	bytesBoard := flag.Bool("bytes", false, "keep the board one byte per cell on one GPU (GOL_LAYOUT_BYTES)")
 	flag.Parse()
-	b, err := golhip.NewBroker(golhip.Config{Device: -1, Shards: *gpus, TurnsPerLaunch: *k})
+	layout := 0
+	if *bytesBoard {
+		layout = golhip.LayoutBytes
+	}
+	b, err := golhip.NewBroker(golhip.Config{Device: -1, Shards: *gpus, TurnsPerLaunch: *k, Layout: layout})
 	if err != nil {
 		fmt.Fprintln(os.Stderr, err)
 		os.Exit(1)

@@ -88,11 +88,15 @@ func PartitionRows(h, n, i int) (int, int, error) {
 	return int(y0), int(y1), nil
 }
 
+// LayoutBytes keeps a Run's board one byte per cell (GOL_LAYOUT_BYTES): one GPU, the byte pipeline.
+const LayoutBytes = int(C.GOL_LAYOUT_BYTES)
+
 // Config selects the broker's GPUs and kernel parameters (gol_config).
 type Config struct {
 	Device         int // first GPU; -1 = current
 	Shards         int // GPUs the board of a Run is row-sharded over (<= 1: one GPU)
 	TurnsPerLaunch int // 0 = library default
+	Layout         int // 0 = automatic (bit board); LayoutBytes = one byte per cell, one GPU
 }
 
 // Broker is the C++ service behind the reference's Operations (broker.go:62-277): the board
@@ -103,7 +107,7 @@ type Broker struct{ b *C.gol_broker }
 func NewBroker(cfg Config) (*Broker, error) {
 	var b *C.gol_broker
 	c := C.gol_config{device: C.int32_t(cfg.Device), turns_per_launch: C.int32_t(cfg.TurnsPerLaunch),
-		shards: C.int32_t(cfg.Shards)}
+		shards: C.int32_t(cfg.Shards), layout: C.int32_t(cfg.Layout)}
 	if err := check(C.gol_broker_create(&c, &b)); err != nil {
 		return nil, err
 	}

@@ -100,7 +100,7 @@ struct Operations {
 
     // The board of a Run: row-sharded over cfg.shards GPUs (broker.go:135-206's split applied
     // to GPUs) when configured and the board allows it (W % 64 == 0, at least one row per
-    // shard), else on one GPU.
+    // shard), else on one GPU (a byte board, GOL_LAYOUT_BYTES, always: it does not shard).
     int ensure_engine(int64_t h, int64_t w)
     {
         if (eng && H == h && W == w) return GOL_OK;
@@ -109,7 +109,7 @@ struct Operations {
         H = h;
         W = w;
         gol_config c = cfg;
-        if (c.shards > 1 && (w % 64 != 0 || h < c.shards)) c.shards = 1;
+        if (c.shards > 1 && (w % 64 != 0 || h < c.shards || c.layout == GOL_LAYOUT_BYTES)) c.shards = 1;
         if (c.shards <= 1) c.transport = GOL_TRANSPORT_AUTO;
         return gol_engine_create(h, w, &c, &eng);
     }

@@ -11,7 +11,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import TRANSPORTS, check, gol_config, gol_request, gol_response, lib
+from ._lib import LAYOUTS, TRANSPORTS, check, gol_config, gol_request, gol_response, lib
 from .stubs import CellList, Request, Response
 
 
@@ -40,11 +40,13 @@ class Operations:
     """broker.go:60 `type Operations struct{}` with its five RPC methods."""
 
     def __init__(self, *, device: int = -1, turns_per_launch: int = 0, cells_per_lane: int = 0, shards: int = 1,
-                 transport: str = "auto", same_device: bool = False):
+                 transport: str = "auto", same_device: bool = False, layout: str = "auto"):
         """shards > 1: the board of a Run is row-sharded over that many GPUs (the reference's
-        Threads split, broker.go:135-206, applied to GPUs), with the same results."""
+        Threads split, broker.go:135-206, applied to GPUs), with the same results.  layout="bytes":
+        the board stays one byte per cell on one GPU (GOL_LAYOUT_BYTES, the byte pipeline)."""
         cfg = gol_config(device=device, turns_per_launch=turns_per_launch, cells_per_lane=cells_per_lane,
-                         shards=shards, transport=TRANSPORTS[transport], flags=1 if same_device else 0)
+                         shards=shards, transport=TRANSPORTS[transport], flags=1 if same_device else 0,
+                         layout=LAYOUTS[layout])
         h = ctypes.c_void_p()
         check(lib().gol_broker_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

@@ -61,6 +61,22 @@ def test_gol_matrix(golhip, golden_dir, size, turns):
 
 
 @pytest.mark.parametrize("size", SIZES)
+def test_gol_matrix_byte_board(golhip, golden_dir, size):
+    """TestGol through a broker that keeps the board one byte per cell (layout="bytes": the
+    byte pipeline for 100 turns), for every turn count of the matrix."""
+    board = _golden_board(golden_dir, size)
+    ops = golhip.Operations(device=0, layout="bytes", shards=2, same_device=True)  # (bytes: one GPU)
+    for turns in TURNS:
+        expected, gold = _golden_alive(golden_dir, size, turns)
+        for threads in (1, 5):
+            res = ops.Run(golhip.Request(World=board, Turns=turns, ImageHeight=size, ImageWidth=size,
+                                         Threads=threads))
+            assert res.TurnsCompleted == turns
+            assert set((c.X, c.Y) for c in res.Alive) == expected, f"{size}x{size}x{turns}-{threads}"
+            assert np.array_equal(res.World, gold)
+
+
+@pytest.mark.parametrize("size", SIZES)
 @pytest.mark.parametrize("turns", TURNS)
 def test_pgm_output(golhip, golden_dir, tmp_path, size, turns):
     """TestPgm: the P5 file written from the device is byte-identical to check/images."""
