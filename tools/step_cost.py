@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--nocount", action="store_true", help="plain steps (no fused alive count)")
     ap.add_argument("--zero", action="store_true", help="an all-dead board (same instructions, no bit toggling)")
-    ap.add_argument("--lib", default="", help="a measurement build of the library (tools/build_variant.sh)")
+    ap.add_argument("--lib", default="", help="a measurement build of the library (tools/variant.sh)")
     a = ap.parse_args()
     import torch
     import golhip
