@@ -15,7 +15,9 @@ class gol_ipc;
 // Library defaults for the bit-board step (chosen from the gfx950 sweep recorded
 // in DESIGN.md; overridable per engine through gol_config).
 #define GOL_DEFAULT_K 8        // standard layout
+#ifndef GOL_DEFAULT_BAND_K
 #define GOL_DEFAULT_BAND_K 12  // band layout, 4 words per lane: the split pipeline
+#endif
 #define GOL_DEFAULT_BYTES_K 32 // byte board: the byte pipeline (0/255 boards with W % 32 == 0)
 #define GOL_DEFAULT_DW 2       // standard layout: 64 cells per lane
 

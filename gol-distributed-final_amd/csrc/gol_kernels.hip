@@ -819,7 +819,9 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
 #endif
 // Pipeline shape of k = 12: KW stages in each of P waves; blocks of GOL_BAND_RPB rows (one pair
 // step), rings of GOL_BAND_NS slots (the role loops are unrolled over the slots).
+#ifndef GOL_BAND_KW
 #define GOL_BAND_KW 3
+#endif
 #define GOL_BAND_P 4
 #define GOL_BAND_RPB 2
 #define GOL_BAND_NS 4
@@ -2603,7 +2605,7 @@ hipError_t golk_band_step(const uint32_t *top, const uint32_t *mid, const uint32
     const bool contig = top + (int64_t)k * pitch == mid && bot == mid + R * pitch;
     const int U = band_useful_words(k, dw);
     a.ngroups = (int)((Wd + U - 1) / U);
-    if (dw == 4 && k == 12) {
+    if (dw == 4 && k == GOL_BAND_KW * GOL_BAND_P) {
         // one workgroup per (column group, strip): strips up to 1024 rows (measured best at k = 12)
         // Boards with fewer than ~256 tiles of 8k rows are latency-bound (a launch lasts one
         // pipeline's walk over strip + 2k rows): ~512 tiles of >= 2 rows instead, without the
@@ -2632,7 +2634,7 @@ int golk_band_useful_words(int k, int dw) { return band_useful_words(k, dw); }
 
 double golk_step_rounds(bool band, int64_t rows, int64_t Wd, int64_t pitch, int k, int dw, int strip)
 {
-    if (!band || dw != 4 || k != 12 || rows <= 0) return 1e9;
+    if (!band || dw != 4 || k != GOL_BAND_KW * GOL_BAND_P || rows <= 0) return 1e9;
     const int64_t ngroups = (Wd + band_useful_words(k, dw) - 1) / band_useful_words(k, dw);
     const int64_t slots = resident_workgroups(golk_band_pipe_fn(true, true), 64 * GOL_BAND_P);
     if (slots <= 0) return 1e9;
