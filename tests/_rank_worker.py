@@ -29,7 +29,7 @@ def main():
     import golhip._lib as L
     lib = L.load(a["lib"]) if a.get("lib") else None
     uid = bytes.fromhex(a["uid"])
-    kw = dict(device=0, transport=a.get("transport", "ipc"), layout=a.get("layout", "auto"),
+    kw = dict(device=a.get("device", 0), transport=a.get("transport", "ipc"), layout=a.get("layout", "auto"),
               turns_per_launch=a.get("k", 0), step=a.get("step", "auto"))
     if lib is not None:
         kw["library"] = lib

@@ -35,9 +35,10 @@ def G():
     return golhip
 
 
-def run_ranks(G, nranks, H, W, scenario, per_rank=None, timeout=150, ipc_timeout_ms=30000, **kw):
+def run_ranks(G, nranks, H, W, scenario, per_rank=None, timeout=150, ipc_timeout_ms=30000, transport="ipc", **kw):
     """Start nranks worker processes (one rank each) and return their JSON results by rank."""
-    uid = G.engine.ipc_unique_id().hex()
+    uid = G.engine.unique_id(transport).hex()
+    kw["transport"] = transport
     env = dict(os.environ, GOL_IPC_TIMEOUT_MS=str(ipc_timeout_ms))
     procs = []
     for r in range(nranks):
@@ -92,6 +93,31 @@ def test_ipc_ranks_match_oracle(G, tmp_path, nranks, H, W, k, turns, every):
         assert d["rows_sha"] == rows_sha(ref[d["y0"]:d["y1"]])
         mine = [[x, y] for x, y in flips if d["y0"] <= y < d["y1"]]
         assert d["flips"] == mine
+        assert d["hash_after_flip"] == O.hash_words(after)
+    assert pgm.read_bytes() == O.pgm_bytes(O.unpack(ref))
+
+
+@pytest.mark.parametrize("H,W,k,turns,every", [(1024, 2048, 0, 37, 5), (515, 4096, 0, 41, 1), (301, 64 * 40, 8, 22, 11)])
+def test_rccl_ranks_match_oracle(G, tmp_path, H, W, k, turns, every):
+    """RCCL between GPUs, one process per GPU as torch.distributed.run starts them (RCCL refuses two
+    ranks on one GPU: needs >= 2 GPUs, skipped on a 1-GPU box): up to 8 ranks, the same checks as
+    the IPC ranks' -- counts, hash, rows, the flipped cells and the P5 file against the oracle."""
+    import torch
+    n = min(torch.cuda.device_count(), 8)
+    if n < 2:
+        pytest.skip("RCCL ranks need >= 2 GPUs")
+    ref, counts = O.bits_run(O.random_words(7, 0, H, W // 64), turns, with_counts=True)
+    pgm = tmp_path / "ranks.pgm"
+    res = run_ranks(G, n, H, W, "random", transport="rccl", per_rank=lambda r: {"device": r}, k=k, seed=7,
+                    turns=turns, every=every, pgm=str(pgm), flips=True)
+    after = O.bits_run(ref, 1)
+    flips = O.flipped_cells(O.unpack(ref), O.unpack(after))
+    for r, d in res.items():
+        assert d["topology"] == {"shards": 1, "nranks": n, "rank": r, "transport": "rccl"}
+        assert d["counts"] == [int(counts[every * (i + 1) - 1]) for i in range(turns // every)]
+        assert d["hash"] == O.hash_words(ref)
+        assert d["rows_sha"] == rows_sha(ref[d["y0"]:d["y1"]])
+        assert d["flips"] == [[x, y] for x, y in flips if d["y0"] <= y < d["y1"]]
         assert d["hash_after_flip"] == O.hash_words(after)
     assert pgm.read_bytes() == O.pgm_bytes(O.unpack(ref))
 
