@@ -825,6 +825,11 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
 #define GOL_BAND_P 4
 #define GOL_BAND_RPB 2
 #define GOL_BAND_NS 4
+// The loader issues block b + GOL_BAND_PREFETCH at block b (its in_ring slot was read at the start
+// of block b + GOL_BAND_PREFETCH - NS, so up to NS) and waits for block b + 1 only.
+#ifndef GOL_BAND_PREFETCH
+#define GOL_BAND_PREFETCH 2
+#endif
 template <int KW, int P, bool CONTIG, bool COUNT>
 __global__ void __launch_bounds__(64 * P)
 __attribute__((amdgpu_waves_per_eu(KW >= 4 ? 3 : 4, 8)))  // 5 KW DW pipeline VGPRs
@@ -1004,10 +1009,14 @@ band_pipe_kernel(BitsArgs a)
     if (wv == 0 && dir && lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
     // block 0's rows, read to completion here (the compiler copies the loop-carried registers
     // on loop entry, which must not happen while a read is in flight)
+    constexpr int PF = GOL_BAND_PREFETCH;
+    static_assert(PF >= 2 && PF <= NS, "blocks b+1 .. b+PF in flight in NS slots");
     if (wv == 0) {
         stage_in(0, in_ring[0]);
         stage_in(1, in_ring[1]);
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        if constexpr (PF > 2) stage_in(2, in_ring[2 % NS]);
+        if constexpr (PF > 3) stage_in(3, in_ring[3 % NS]);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RPB * (PF - 1)) : "memory");  // block 0 (and the claim)
     } else if (seen_ready < 1) {
         seen_ready = spin_until_ge(ready_l + wv, 1);
         if (seen_ready < 0) {
@@ -1064,10 +1073,9 @@ band_pipe_kernel(BitsArgs a)
         // block b+1's rows: read now, waited for at the next block's start (the compute of the
         // other waves of the SIMD covers the LDS latency)
         if constexpr (ROLE == 0) {
-            stage_in(b + 2, in_ring[(US + 2) % NS]);  // refills block b-2's slot (clamped past the end)
-            // block b+1 landed, b+2 in flight (and, paired, at US 1 the claim issued at US 0)
-            if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            stage_in(b + PF, in_ring[(US + PF) % NS]);  // refills block b+PF-NS's slot (clamped past the end)
+            // block b+1 landed, b+2 .. b+PF in flight (and, paired, at US 1 the claim issued at US 0)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RPB * (PF - 1) + (DYN && US == 1 ? 1 : 0)) : "memory");
             if constexpr (DYN && US == 0) {
                 if (lane == 0) pending = atomicAdd(ctr, (uint32_t)NS);
             }
