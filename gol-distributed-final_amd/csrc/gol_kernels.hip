@@ -826,9 +826,11 @@ __device__ __forceinline__ int claim_cu_slot(uint32_t *m)
 #define GOL_BAND_RPB 2
 #define GOL_BAND_NS 4
 // The loader issues block b + GOL_BAND_PREFETCH at block b (its in_ring slot was read at the start
-// of block b + GOL_BAND_PREFETCH - NS, so up to NS) and waits for block b + 1 only.
+// of block b + GOL_BAND_PREFETCH - NS, so up to NS) and waits for block b + 1 only.  Same box, 3
+// reps: 3 against 2 weak 163.6-164.1 vs 163.1-163.7 TCUPS, 262144^2 +0.6 %, 65536^2 +1.2 %; 4 as 3
+// (profiles/r05/r05d_ab_prefetch.jsonl).
 #ifndef GOL_BAND_PREFETCH
-#define GOL_BAND_PREFETCH 2
+#define GOL_BAND_PREFETCH 3
 #endif
 template <int KW, int P, bool CONTIG, bool COUNT>
 __global__ void __launch_bounds__(64 * P)
