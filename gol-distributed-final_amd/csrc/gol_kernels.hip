@@ -623,6 +623,9 @@ __global__ void __launch_bounds__(256) band_step_kernel(BitsArgs a)
 // flight as a pending LDS write and would put vmcnt(0) before every LDS access it can see
 // (which, on the storing wave, also waits for its HBM stores).
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// ceil(a / d) for a >= 0 (else 0) and floor(a / d) for any a (d > 0)
+__device__ __forceinline__ int div_ceil_nn(int a, int d) { return a > 0 ? (a + d - 1) / d : 0; }
+__device__ __forceinline__ int div_floor(int a, int d) { return a >= 0 ? a / d : -((-a + d - 1) / d); }
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u32;
 __device__ __forceinline__ v4u32 lds_rd128(const lds_u32 *p)
 {
@@ -894,21 +897,23 @@ band_pipe_kernel(BitsArgs a)
     // own rows: every block but the first and last few of a strip) take the row address carried
     // from the previous block (uniform) plus the lane's offset; the others clamp and pick the row's
     // segment per row.  stage_in is called for blocks 0, 1, 2, ... in order.
+    // The slot is an LDS-typed pointer (a generic one costs a null check per load: 4 SALU).  The
+    // interior blocks are one range [ib_lo, ib_lo + ib_n) of block numbers, found here once.
     const int in_lo = CONTIG ? first_in : max(first_in, 0), in_hi = CONTIG ? last_in : min(last_in, R - 1);
     const int64_t row_step = dir >= 0 ? (int64_t)pitch_b : -(int64_t)pitch_b;
-    int st_y = dir >= 0 ? first_in : s1e + K - 1;  // first row of the next block
-    const char *st_row = mid_b + (int64_t)st_y * pitch_b;  // its address (used when interior)
-    auto stage_in = [&](int b, uint32_t (*slot)[ROW]) {
-        const int y0 = st_y;
+    const int y_first = dir >= 0 ? first_in : s1e + K - 1;  // first row of block 0
+    const int ib_lo = dir >= 0 ? div_ceil_nn(in_lo - y_first, RPB) : div_ceil_nn(y_first - in_hi, RPB);
+    const int ib_hi = dir >= 0 ? div_floor(in_hi - (RPB - 1) - y_first, RPB) : div_floor(y_first - (RPB - 1) - in_lo, RPB);
+    const uint32_t ib_n = ib_hi >= ib_lo ? (uint32_t)(ib_hi - ib_lo + 1) : 0u;
+    const char *st_row = mid_b + (int64_t)y_first * pitch_b;  // the next block's first row (used when interior)
+    auto stage_in = [&](int b, lds_u32 *slot) {
         const char *g0 = st_row;
-        st_y += dir >= 0 ? RPB : -RPB;
         st_row += RPB * row_step;
-        const int ylo = dir >= 0 ? y0 : y0 - (RPB - 1), yhi = dir >= 0 ? y0 + (RPB - 1) : y0;
-        if (ylo >= in_lo && yhi <= in_hi) {
+        if ((uint32_t)(b - ib_lo) < ib_n) {
 #pragma unroll
             for (int s = 0; s < RPB; ++s)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g0 + s * row_step + lane_off), &slot[s][0], 16, 0,
-                                                 GOL_BAND_LOAD_AUX);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g0 + s * row_step + lane_off), slot + s * ROW, 16,
+                                                 0, GOL_BAND_LOAD_AUX);
             return;
         }
 #pragma unroll
@@ -918,7 +923,7 @@ band_pipe_kernel(BitsArgs a)
             y = y > last_in ? last_in : (y < first_in ? first_in : y);
             const int64_t d = CONTIG ? 0 : (y < 0 ? top_d : (y >= R ? bot_d : 0));
             const char *g = mid_b + (d + (int64_t)y * pitch_b) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), &slot[s][0], 16, 0, GOL_BAND_LOAD_AUX);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), slot + s * ROW, 16, 0, GOL_BAND_LOAD_AUX);
         }
     };
 
@@ -1014,10 +1019,10 @@ band_pipe_kernel(BitsArgs a)
     constexpr int PF = GOL_BAND_PREFETCH;
     static_assert(PF >= 2 && PF <= NS, "blocks b+1 .. b+PF in flight in NS slots");
     if (wv == 0) {
-        stage_in(0, in_ring[0]);
-        stage_in(1, in_ring[1]);
-        if constexpr (PF > 2) stage_in(2, in_ring[2 % NS]);
-        if constexpr (PF > 3) stage_in(3, in_ring[3 % NS]);
+        stage_in(0, in_l);
+        stage_in(1, in_l + SLOT);
+        if constexpr (PF > 2) stage_in(2, in_l + (2 % NS) * SLOT);
+        if constexpr (PF > 3) stage_in(3, in_l + (3 % NS) * SLOT);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RPB * (PF - 1)) : "memory");  // block 0 (and the claim)
     } else if (seen_ready < 1) {
         seen_ready = spin_until_ge(ready_l + wv, 1);
@@ -1075,7 +1080,7 @@ band_pipe_kernel(BitsArgs a)
         // block b+1's rows: read now, waited for at the next block's start (the compute of the
         // other waves of the SIMD covers the LDS latency)
         if constexpr (ROLE == 0) {
-            stage_in(b + PF, in_ring[(US + PF) % NS]);  // refills block b+PF-NS's slot (clamped past the end)
+            stage_in(b + PF, in_l + ((US + PF) % NS) * SLOT);  // refills block b+PF-NS's slot (clamped past the end)
             // block b+1 landed, b+2 .. b+PF in flight (and, paired, at US 1 the claim issued at US 0)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RPB * (PF - 1) + (DYN && US == 1 ? 1 : 0)) : "memory");
             if constexpr (DYN && US == 0) {
@@ -1492,21 +1497,26 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
     // shard and inside [first_in, last_in]: every block but the first and last few of a strip) take
     // one row address, carried from block to block and stepped by a pitch; the others clamp and
     // pick the row's segment per row (round 4: +2.4 % on 16384^2 bytes over per-row addresses).
+    // The slot is an LDS-typed pointer (a generic one costs a null check per load: 4 SALU) and the
+    // interior blocks are one range [ib_lo, ib_lo + ib_n) of block numbers, found here once.  (The
+    // load's immediate offset moves its LDS destination too: the second 16 bytes of a lane's 32
+    // take their own address.)
     const int in_lo = max(first_in, 0), in_hi = min(last_in, R - 1);
     const int64_t row_step = dir >= 0 ? (int64_t)pitch : -(int64_t)pitch;
-    int st_y = in_row(0);
-    const char *st_g = mid_b + (int64_t)st_y * pitch + lane_off;
-    auto stage_in = [&](int b, uint32_t (*slot)[2][256]) {
-        const int y0 = st_y;
+    const int y_first = in_row(0);
+    const int ib_lo = dir >= 0 ? div_ceil_nn(in_lo - y_first, RPB) : div_ceil_nn(y_first - in_hi, RPB);
+    const int ib_hi = dir >= 0 ? div_floor(in_hi - (RPB - 1) - y_first, RPB) : div_floor(y_first - (RPB - 1) - in_lo, RPB);
+    const uint32_t ib_n = ib_hi >= ib_lo ? (uint32_t)(ib_hi - ib_lo + 1) : 0u;
+    const char *st_g = mid_b + (int64_t)y_first * pitch + lane_off;
+    constexpr int IROW = 2 * 256;  // uint32 per input row in LDS (two 16-byte halves of 64 lanes)
+    auto stage_in = [&](int b, lds_u32 *slot) {
         const char *g = st_g;
-        st_y += dir >= 0 ? RPB : -RPB;
         st_g += RPB * row_step;
-        const int ylo = dir >= 0 ? y0 : y0 - (RPB - 1), yhi = dir >= 0 ? y0 + (RPB - 1) : y0;
-        if (ylo >= in_lo && yhi <= in_hi) {
+        if ((uint32_t)(b - ib_lo) < ib_n) {
 #pragma unroll
             for (int S = 0; S < RPB; ++S) {
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step), &slot[S][0][0], 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), &slot[S][1][0], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step), slot + S * IROW, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), slot + S * IROW + 256, 16, 0, 0);
             }
             return;
         }
@@ -1516,8 +1526,8 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
             y = y > last_in ? last_in : (y < first_in ? first_in : y);  // past the end: clamped, never stored
             const int64_t d = y < 0 ? top_d : (y >= R ? bot_d : 0);
             const char *gg = mid_b + (d + (int64_t)y * pitch) + lane_off;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg), &slot[S][0][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg + 16), &slot[S][1][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg), slot + S * IROW, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gg + 16), slot + S * IROW + 256, 16, 0, 0);
         }
     };
     __builtin_amdgcn_s_setprio(1);  // polls drop to 0 (spin_until_ge<true>)
@@ -1612,8 +1622,8 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
         for (int h = 0; h < 2 * RPB; ++h) lds_settle<0>(nb[h]);
     };
     if (wv == 0) {
-        stage_in(0, in_ring[0]);
-        stage_in(1, in_ring[1]);
+        stage_in(0, in_l);
+        stage_in(1, in_l + ISLOT);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RPB) : "memory");  // block 0 landed (the claim before it too)
 #pragma unroll
         for (int S = 0; S < RPB; ++S) nw[S] = 0;
@@ -1680,7 +1690,7 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
         }
         // block b+1's rows: read now, waited for at the next block's start
         if constexpr (ROLE == 0) {
-            stage_in(b + 2, in_ring[(US + 2) % NSI]);  // refills block b+2-NSI's slot (clamped past the end)
+            stage_in(b + 2, in_l + ((US + 2) % NSI) * ISLOT);  // refills block b+2-NSI's slot (clamped past the end)
             // block b+1 landed, b+2 in flight (2 RPB loads; and, paired, at US 1 the claim issued at US 0)
             if constexpr (DYN && US == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RPB + 1) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RPB) : "memory");
