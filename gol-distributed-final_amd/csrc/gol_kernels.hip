@@ -1268,19 +1268,18 @@ __device__ __forceinline__ uint32_t pack32(const uint4 lo, const uint4 hi)
     return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
 }
 // Same for bytes that are exactly 0x00 or 0xFF (-1 as int8): weights -2^i give +2^i per set byte.
-// The VOP3P v_dot4_i32_i8 (a separate accumulator operand, 0 inline) written out: the builtin
-// becomes v_mov 0 + two dependent v_dot4c per byte and an `s_nop 2` before the result is used
-// (byte pipeline loader: +1.5 % on 16384^2, profiles/r05/r05e_ab_bytes_dot_sched.jsonl).
+// (Builtins, not inline asm: a v_dot4 result read by another VALU needs 3 wait states, which the
+// compiler's hazard recognizer inserts only for instructions it can see.  The inline-asm VOP3P
+// form measured +1.5 % and then +-0 on another box, and under the post-RA scheduler it read
+// stale sums: profiles/r05/r05y_ab_bytes_sched.jsonl.)
 __device__ __forceinline__ uint32_t pack32_ff(const uint4 lo, const uint4 hi)
 {
     const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     uint32_t b[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t h;
-        asm("v_dot4_i32_i8 %0, %1, %2, 0" : "=v"(h) : "v"(d[2 * q + 1]), "v"(0x80C0E0F0u));
-        asm("v_dot4_i32_i8 %0, %1, %2, %3" : "=v"(b[q]) : "v"(d[2 * q]), "v"(0xF8FCFEFFu), "v"(h));
-    }
+    for (int q = 0; q < 4; ++q)
+        b[q] = (uint32_t)__builtin_amdgcn_sdot4((int)d[2 * q], (int)0xF8FCFEFFu,
+                                               __builtin_amdgcn_sdot4((int)d[2 * q + 1], (int)0x80C0E0F0u, 0, false), false);
     return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
 }
 
