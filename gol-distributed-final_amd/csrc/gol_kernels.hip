@@ -675,6 +675,24 @@ __device__ __forceinline__ uint32_t lds_rd32_issue_o(const lds_u32 *p)
     asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(p), "i"(OFF) : "memory");
     return r;
 }
+// Two-instruction forms (one asm statement: one conservative hazard s_nop after it, not two):
+// the band pipeline's block reads, writes, settle and middle-wave flags through these measured
+// weak 163.3 -> 165.2 TCUPS, 262144^2 +0.2 % (same box, profiles/r05/r05g_ab_lds_pairs.jsonl).
+template <int OFF0, int OFF1>
+__device__ __forceinline__ void lds_rd128x2_issue_o(const lds_u32 *p, v4u32 &a, v4u32 &b)
+{
+    asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4" : "=&v"(a), "=&v"(b) : "v"(p), "i"(OFF0), "i"(OFF1) : "memory");
+}
+template <int OFF0, int OFF1>
+__device__ __forceinline__ void lds_wr128x2_o(lds_u32 *p, v4u32 a, v4u32 b)
+{
+    asm volatile("ds_write_b128 %0, %1 offset:%3\n\tds_write_b128 %0, %2 offset:%4" ::"v"(p), "v"(a), "v"(b), "i"(OFF0), "i"(OFF1) : "memory");
+}
+__device__ __forceinline__ void lds_settle2(v4u32 &a, v4u32 &b) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory"); }
+__device__ __forceinline__ void lds_flag_wr2(lds_u32 *p, int v, lds_u32 *q, int w)
+{
+    asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3" ::"v"(p), "v"(v), "v"(q), "v"(w) : "memory");
+}
 // Flag write without an exec mask: lane 0's address is the flag, the other lanes write their
 // own scratch word (one ds_write, no saveexec / branch around it).
 __device__ __forceinline__ void lds_flag_wr(lds_u32 *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory"); }
@@ -1047,12 +1065,12 @@ band_pipe_kernel(BitsArgs a)
         uint32_t r0[DW], r1[DW];
         // block b's rows, the youngest LDS operations of this wave: once they are in, so are
         // block b-1's row writes, and both flags can go out at once
-        lds_settle<0>(nx0);
-        lds_settle<0>(nx1);
+        lds_settle2(nx0, nx1);
         unpack(nx0, r0);
         unpack(nx1, r1);
-        if constexpr (ROLE != 0) lds_flag_wr(cns_addr, b + 1);  // block b's slot is free
-        if constexpr (!LAST) lds_flag_wr(rdy_addr, b);          // blocks < b are in ring wv+1
+        if constexpr (ROLE == 1) lds_flag_wr2(cns_addr, b + 1, rdy_addr, b);
+        else if constexpr (ROLE != 0) lds_flag_wr(cns_addr, b + 1);  // block b's slot is free
+        else lds_flag_wr(rdy_addr, b);          // blocks < b are in ring wv+1
         if constexpr (ROLE == 0) {
             if (wrap) {
 #pragma unroll
@@ -1074,8 +1092,7 @@ band_pipe_kernel(BitsArgs a)
                 seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);
                 if (seen_free < 0) return false;
             }
-            lds_wr128_o<US * SB>(wr_base, pack(r0));
-            lds_wr128_o<US * SB + RB>(wr_base, pack(r1));
+            lds_wr128x2_o<US * SB, US * SB + RB>(wr_base, pack(r0), pack(r1));
         }
         // block b+1's rows: read now, waited for at the next block's start (the compute of the
         // other waves of the SIMD covers the LDS latency)
@@ -1094,8 +1111,7 @@ band_pipe_kernel(BitsArgs a)
             }
             more = seen_ready < FINAL || b + 1 < seen_ready - FINAL;
         }
-        nx0 = lds_rd128_issue_o<NXT * SB>(src_base);  // (past the stream's end: a stale slot, unused)
-        nx1 = lds_rd128_issue_o<NXT * SB + RB>(src_base);
+        lds_rd128x2_issue_o<NXT * SB, NXT * SB + RB>(src_base, nx0, nx1);  // (past the stream's end: a stale slot, unused)
         return true;
     };
     // blocks the loader has: nblkT, or (paired) the claims granted so far
