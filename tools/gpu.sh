@@ -13,6 +13,8 @@
 #   tools/gpu.sh ab BASE "bench args;..."   same-box A/B of tools/variants/libBASE.so against the product
 #   tools/gpu.sh share                      the several-process (IPC) rank tests + --share-gpu bench lines
 #   tools/gpu.sh final TAG                  suite, profile TAG, clock (if built), bench: a round's evidence
+#   tools/gpu.sh driver                     the driver's bench command twice + once under rocprofv3 --stats
+#                                           (gpurun_out/drv/: bench_1/2.json, bench_trace.json, trace/)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
@@ -83,6 +85,16 @@ share() {
   tail -4 gpurun_out/share.jsonl
 }
 
+driver() {  # the round-end driver's own command (bench.py --gpus 1 --steps 20 --warmup 5)
+  mkdir -p gpurun_out/drv
+  for i in 1 2; do
+    timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/drv/bench_$i.json 2> gpurun_out/drv/bench_$i.err || { tail -20 gpurun_out/drv/bench_$i.err; exit 5; }
+  done
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/drv/trace -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $R/gpurun_out/drv/bench_trace.json 2> $R/gpurun_out/drv/bench_trace.err) || exit 6
+  python3 -c "import json; [print(f, json.load(open('gpurun_out/drv/%s.json' % f))['value']) for f in ('bench_1', 'bench_2', 'bench_trace')]"
+}
+
 cmd=${1:-suite}; shift || true
 case $cmd in
   suite) tests tests ${1:+-k "$1"} && smoke && bench_default ;;
@@ -93,6 +105,7 @@ case $cmd in
   clock) clock "$@" ;;
   ab) ab "$@" ;;
   share) share ;;
+  driver) driver ;;
   final)
     tag=${1:?tag}
     tests tests && smoke && profile $tag && { [ ! -f tools/variants/libclock.so ] || clock; } && bench_default ;;
