@@ -200,3 +200,12 @@ def test_go_shims_use_only_declared_c_symbols():
     struct_text = " ".join(re.findall(r"typedef struct gol_(?:config|request|response) \{(.*?)\}", header, re.S))
     for f in fields:
         assert re.search(r"\b%s\b" % f, struct_text), f
+
+
+def test_layout_constants_match_header(G):
+    """gol_config.layout values (golhip.h) and the binding's names agree, GOL_LAYOUT_BYTES
+    included (round 5: the byte board as a layout)."""
+    text = open(HEADER).read()
+    vals = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define GOL_LAYOUT_([A-Z]+) (\d+)", text)}
+    assert vals == {"AUTO": 0, "STANDARD": 1, "BAND": 2, "BYTES": 3}
+    assert G._lib.LAYOUTS == {k.lower(): v for k, v in vals.items()}
