@@ -47,6 +47,9 @@ BYTES_BYTES_PER_UPDATE = 2.0  # 1 byte read + 1 byte written
 # the kernel sources and the flags they are compiled with (a PMC profile is keyed to their hash)
 KERNEL_SRCS = [os.path.join(ROOT, "gol-distributed-final_amd", "csrc", f)
                for f in ("gol_kernels.hip", "gol_band_pipe.hip", "gol_bytes_pipe.hip", "Makefile")]
+# reference alive-count series of the bench boards (tools/make_bench_counts.py: one GPU, one shard,
+# no exchange); every count of a run is checked against them (`parity` in the line)
+COUNTS_FIXTURE = os.path.join(ROOT, "tests", "golden", "bench_counts.json")
 # nominal rates of the settle steps (bench.py --settle-s): ~the measured 1-GPU rates
 SETTLE_RATE_BITS = 145e12
 SETTLE_RATE_BYTES = 58e12
@@ -88,6 +91,7 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration only (no GPU): ranks, barriers and the JSON line, value 0")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank exits at once
+    ap.add_argument("--library", default="", help=argparse.SUPPRESS)  # tests: another build of libgolhip.so
     a = ap.parse_args(argv)
     # per-workload defaults: each timed region and each warmup >= ~0.1-0.25 s of GPU work
     steps, warm = {"weak": (20, 20), "strong262k": (40, 20), "bit64k": (300, 100), "byte16k": (600, 200)}[a.workload]
@@ -236,6 +240,39 @@ def load_pmc(key):
     return e, e.get("profile")
 
 
+def parity(ranks, board, every, series):
+    """Every alive count of this run (settle, warmup and timed steps: after turns every, 2 every,
+    ...) against the reference series of the same board (COUNTS_FIXTURE), on every rank; FAIL on
+    any rank fails the line.  With N > 1 ranks this is the check that the sharded path (RCCL halo
+    exchange over xGMI, or IPC) computed the same torus as one GPU stepping it whole."""
+    ref = None
+    try:
+        with open(COUNTS_FIXTURE) as f:
+            ref = json.load(f)["boards"].get(board)
+    except (OSError, ValueError, KeyError):
+        pass
+    series = [int(c) for c in series]
+    if not ref or ref.get("every") != every:
+        mine = {"status": "unpinned", "reason": f"no reference series for {board} every {every} turns"}
+    else:
+        want = ref["counts"]
+        n = min(len(want), len(series))
+        bad = next((i for i in range(n) if series[i] != want[i]), None)
+        if bad is not None:
+            mine = {"status": "FAIL", "turn": (bad + 1) * every, "got": series[bad], "want": want[bad]}
+        else:
+            mine = {"status": "ok" if n == len(series) else "partial", "points": n, "turns_checked": n * every,
+                    "turns_done": len(series) * every}
+    allr = ranks.gather(mine)
+    worst = next((r for r in allr if r["status"] == "FAIL"), None) or \
+        next((r for r in allr if r["status"] != "ok"), None) or mine
+    out = dict(worst)
+    out["reference"] = f"tests/golden/bench_counts.json[{board}] (one GPU, one shard, no exchange)"
+    if ranks.world > 1:
+        out["ranks"] = [r["status"] for r in allr]
+    return out
+
+
 def roofline(kind, launch_ms, cell_updates, pmc, pmc_note):
     """The dominant kernel against its binding roof.  With k turns per launch the bit-board step
     is bound by VALU issue: frac = wave64 VALU instructions per launch (PMC
@@ -336,16 +373,19 @@ def run_bits(args, ranks):
     info = e.info()
     k = info["turns_per_launch"]
     e.load_random(1)
-    settle = settle_steps(args, lambda n: e.step_counted(n * k, k), float(H // ranks.world if sharded else H) * W * k,
-                          SETTLE_RATE_BITS)
+    series = []  # every alive count of the run, for the parity check
+
+    def run_n(n):
+        series.extend(e.step_counted(n * k, k).tolist())
+    settle = settle_steps(args, run_n, float(H // ranks.world if sharded else H) * W * k, SETTLE_RATE_BITS)
     several = sharded and world > 1
-    x = {"exchanges": 0, "mean_ms": 0.0}
+    x = {"exchanges": 0, "mean_ms": 0.0, "wait_ms": 0.0, "transfer_ms": 0.0}
     if args.warmup:
         # several ranks: the halo exchanges are timed during the warmup steps (the same work), so
-        # that their event pairs stay out of the timed region
+        # that their events stay out of the timed region
         if several:
             e.set_timing(True, exchanges=True)
-        e.step_counted(args.warmup * k, k)
+        run_n(args.warmup)
         if several:
             x = e.exchange_timing()
             e.set_timing(False)
@@ -357,8 +397,10 @@ def run_bits(args, ranks):
     ranks.barrier()
     t = e.timing()
     e.set_timing(False)
+    series.extend(counts.tolist())
     per_rank = rank_stats(ranks, dt, t, x, topo)
     dt = ranks.max(dt)
+    par = parity(ranks, f"{H}x{W}", k, series)
     alive = int(counts[-1]) if len(counts) else None
     if not sharded and world > 1:
         cells_total = ranks.sum(H * W)  # independent replicas
@@ -390,7 +432,7 @@ def run_bits(args, ranks):
            "transport": topo["transport"], "turns_per_step": k, "layout": layout,
            "cells_per_lane": info["cells_per_lane"], "strip_rows": args.strip or "auto",
            "alive_count_every_step": True, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
-           "settle_steps": settle, "timed_launches": t["launches"]}
+           "settle_steps": settle, "timed_launches": t["launches"], "parity": par}
     if world > 1:
         cfg["rank_stats"] = per_rank
     if snap:
@@ -409,18 +451,23 @@ def rank_stats(ranks, wall_s, timing, xtiming, topo):
     warmup steps, so that no per-exchange event sits in the timed region), of the wall time, and
     the rank count each rank's engine reports (RCCL / IPC nranks) with its transport."""
     mine = {"launch_ms": timing["mean_ms"], "exchange_ms": xtiming["mean_ms"], "exchanges": xtiming["exchanges"],
+            "exchange_wait_ms": xtiming.get("wait_ms", 0.0), "exchange_transfer_ms": xtiming.get("transfer_ms", 0.0),
             "wall_ms": wall_s * 1e3, "nranks": topo["nranks"], "transport": topo["transport"]}
     allr = ranks.gather(mine)
 
     def mm(key):
         v = [r[key] for r in allr]
         return {"max": round(max(v), 4), "min": round(min(v), 4)}
-    return {"launch_ms": mm("launch_ms"), "exchange_ms": mm("exchange_ms"), "wall_ms": mm("wall_ms"),
+    return {"launch_ms": mm("launch_ms"), "exchange_ms": mm("exchange_ms"),
+            "exchange_wait_ms": mm("exchange_wait_ms"), "exchange_transfer_ms": mm("exchange_transfer_ms"),
+            "wall_ms": mm("wall_ms"),
             "exchanges_per_rank": [r["exchanges"] for r in allr], "nranks_seen": [r["nranks"] for r in allr],
             "transports": sorted({r["transport"] for r in allr}),
             "basis": "per rank: launch_ms = mean step time of its shard over the timed steps (HIP events on the compute "
-                     "stream), exchange_ms = mean halo exchange over the warmup steps (event pair on the exchange's "
-                     "stream); max / min over ranks"}
+                     "stream), exchange_ms = mean halo exchange over the warmup steps (events on the exchange's "
+                     "stream) = exchange_wait_ms (waiting for the ring neighbours to reach the exchange: IPC READY "
+                     "polls; RCCL a one-word send/recv with each neighbour issued first while timed) + "
+                     "exchange_transfer_ms (the halo rows); max / min over ranks"}
 
 
 def settle_steps(args, run_n, cell_updates_per_step, nominal_rate):
@@ -447,9 +494,13 @@ def run_bytes(args, ranks):
     assert info["layout"] == "bytes", info
     k = info["turns_per_launch"]
     e.load_random(1)
-    settle = settle_steps(args, lambda n: e.step_counted(n * k, k), float(H) * W * k, SETTLE_RATE_BYTES)
+    series = []
+
+    def run_n(n):
+        series.extend(e.step_counted(n * k, k).tolist())
+    settle = settle_steps(args, run_n, float(H) * W * k, SETTLE_RATE_BYTES)
     if args.warmup:
-        e.step_counted(args.warmup * k, k)
+        run_n(args.warmup)
     ranks.barrier()
     e.set_timing(True)
     t0 = time.perf_counter()
@@ -459,6 +510,8 @@ def run_bytes(args, ranks):
     t = e.timing()
     e.set_timing(False)
     e.close()
+    series.extend(counts.tolist())
+    par = parity(ranks, f"{H}x{W}", k, series)
     dt = ranks.max(dt)
     value = H * W * ranks.world * k * args.steps / dt
     alive = int(counts[-1]) if len(counts) else None
@@ -469,7 +522,7 @@ def run_bytes(args, ranks):
     cfg = {"workload": "byte-16384x16384", "H": H, "W": W, "turns_per_step": k, "layout": "bytes",
            "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "1gpu",
            "alive_count_every_step": True, "alive_final": alive, "turns_done": (settle + args.warmup + args.steps) * k,
-           "settle_steps": settle}
+           "settle_steps": settle, "parity": par}
     return value, dt, cfg, roof, "u8 (byte per cell)"
 
 
@@ -484,12 +537,16 @@ def main():
         args.k = 32  # pipelined byte kernel, 8 waves x 4 turns
     if int(os.environ.get("RANK", "0")) == args.fail_rank:
         sys.exit(3)  # (tests/test_bench_cpu.py: the other ranks wait in a collective for it)
+    if args.library:  # (tests: a fault-injection build must fail the line's parity check)
+        import golhip
+        golhip._lib._lib = golhip._lib.load(os.path.abspath(args.library))
     ranks = Ranks(args)
     if args.dry_run:
         ranks.barrier()
         wall = 0.001 * (ranks.rank + 1)
         fake_t = {"mean_ms": wall * 1e3 / max(args.steps, 1), "launches": args.steps}
-        fake_x = {"mean_ms": 0.01 * (ranks.rank + 1), "exchanges": args.warmup if ranks.world > 1 else 0}
+        fake_x = {"mean_ms": 0.01 * (ranks.rank + 1), "exchanges": args.warmup if ranks.world > 1 else 0,
+                  "wait_ms": 0.004 * (ranks.rank + 1), "transfer_ms": 0.006 * (ranks.rank + 1)}
         per_rank = rank_stats(ranks, wall, fake_t, fake_x, {"nranks": ranks.world, "transport": "dry-run"})
         dt = ranks.max(wall)
         value, cfg, roof, dtype = 0.0, {"workload": "dry-run", "ranks": ranks.world}, None, None
@@ -511,6 +568,8 @@ def main():
                 "config": cfg, "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     ranks.close()
+    if cfg.get("parity", {}).get("status") == "FAIL":
+        sys.exit(1)  # a board that differs from the reference is not a measurement
 
 
 if __name__ == "__main__":

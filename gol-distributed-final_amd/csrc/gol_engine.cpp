@@ -162,6 +162,7 @@ static int shard_alloc(gol_engine *e, gol_shard &s)
     } else {
         for (auto &b : s.bytes) HIPCHK(hipMalloc(&b, e->H * e->bstride));
         HIPCHK(hipMemsetAsync(s.bytes[0], 0, e->H * e->bstride, s.stream));
+        e->bytes_binary = true;  // an all-dead board: 0/255 only
     }
     HIPCHK(hipStreamSynchronize(s.stream));
     return GOL_OK;
@@ -507,6 +508,15 @@ static int plan_of(gol_engine *e, int i, gol_halo_op (&ops)[4])
 {
     int32_t n = 0;
     RCCHK(gol_halo_plan(e->H, e->nranks, e->rank + i, e->kx, ops, 4, &n));
+#ifdef GOL_TEST_MISPAIR
+    // Test build only (make mispair -> libgolhip_mispair.so, tests/test_gpu_ranks.py): the rows
+    // received from below land in the ghost rows above and vice versa -- a mis-paired halo that
+    // bench.py's parity check must catch.
+    int r[2], nr = 0;
+    for (int j = 0; j < 4; ++j)
+        if (ops[j].kind == GOL_HALO_RECV && nr < 2) r[nr++] = j;
+    if (nr == 2) std::swap(ops[r[0]].row, ops[r[1]].row);
+#endif
     return n == 4 ? GOL_OK : gol_set_error(GOL_EINVAL, "halo plan of %d ops", n);
 }
 
@@ -528,6 +538,8 @@ static bool local_wrap(const gol_engine *e)
 }
 
 static int xtime_start(gol_engine *e, gol_shard &s, hipStream_t st, size_t *ev);
+static int xtime_wait(gol_shard &s, hipStream_t st, size_t ev);
+static int xtime_waited(gol_shard &s, hipStream_t st, size_t ev);
 static int xtime_stop(gol_engine *e, gol_shard &s, hipStream_t st, size_t ev, int shard);
 
 // IPC transport (one shard per process): this rank's exchange xn on its comm stream, pulling
@@ -563,7 +575,9 @@ static int exchange_ipc(gol_engine *e)
                                   hipMemcpyDeviceToDevice, s.comm));
         }
     RCCHK(e->ipc->signal(s.comm, GOL_IPC_READY, xn));
+    RCCHK(xtime_wait(s, s.comm, xev));
     RCCHK(e->ipc->wait(s.comm, e->ipc_peers, GOL_IPC_READY, xn, s.err));
+    RCCHK(xtime_waited(s, s.comm, xev));
     for (int j = 0; j < 4; ++j) {
         const gol_halo_op &rv = mine[j];
         if (rv.kind != GOL_HALO_RECV) continue;
@@ -627,7 +641,11 @@ static int exchange(gol_engine *e, bool on_compute = false)
                 }
                 if (!sd || sd->rows != rv.rows) return gol_set_error(GOL_EINVAL, "halo plan: unmatched receive");
                 gol_shard &ps = e->sh[p];
-                if (xev == SIZE_MAX) RCCHK(xtime_start(e, s, s.comm, &xev));
+                if (xev == SIZE_MAX) {  // (the peers' rows are in once the event waits above pass: no wait here)
+                    RCCHK(xtime_start(e, s, s.comm, &xev));
+                    RCCHK(xtime_wait(s, s.comm, xev));
+                    RCCHK(xtime_waited(s, s.comm, xev));
+                }
                 RCCHK(copy_rows(s, s.bits[c] + rv.row * P, ps, ps.bits[c] + sd->row * P, hb, s.comm));
             }
             RCCHK(xtime_stop(e, s, s.comm, xev, i));
@@ -648,11 +666,40 @@ static int exchange(gol_engine *e, bool on_compute = false)
             HIPCHK(hipStreamWaitEvent(s.comm, s.ev_edge, 0));
         }
     std::vector<size_t> xev(n);
+    bool timed = false;
     for (int i = 0; i < n; ++i) {
         RCCHK(set_dev(e->sh[i].device));
         RCCHK(xtime_start(e, e->sh[i], xs(e->sh[i]), &xev[i]));
+        RCCHK(xtime_wait(e->sh[i], xs(e->sh[i]), xev[i]));
+        timed |= xev[i] != SIZE_MAX;
     }
-    ncclResult_t first = ncclGroupStart();
+    ncclResult_t first = ncclSuccess;
+    if (timed) {
+        // Only while exchanges are timed (gol_engine_exchange_split): one word to and from each
+        // distinct ring neighbour first.  It completes once every neighbour has reached its
+        // exchange, so its duration is this rank's wait for them and the group after it is the
+        // transfer of the halo rows.  (Device words coll[8..10]: not used by the agreement.)
+        first = ncclGroupStart();
+        for (int i = 0; i < n && first == ncclSuccess; ++i) {
+            gol_shard &s = e->sh[i];
+            int peers[4], np = 0;
+            for (const auto &op : plans[i])
+                if (std::find(peers, peers + np, op.peer) == peers + np) peers[np++] = op.peer;
+            for (int j = 0; j < np; ++j) {
+                ncclResult_t x = ncclSend(s.coll + 8, 1, ncclUint32, peers[j], s.nccl, xs(s));
+                if (x == ncclSuccess) x = ncclRecv(s.coll + 9 + (j & 1), 1, ncclUint32, peers[j], s.nccl, xs(s));
+                if (x != ncclSuccess && first == ncclSuccess) first = x;
+            }
+        }
+        const ncclResult_t end = ncclGroupEnd();
+        if (first != ncclSuccess || end != ncclSuccess)
+            return gol_set_error(GOL_ECOMM, "halo handshake: %s", ncclGetErrorString(first != ncclSuccess ? first : end));
+    }
+    for (int i = 0; i < n; ++i) {
+        RCCHK(set_dev(e->sh[i].device));
+        RCCHK(xtime_waited(e->sh[i], xs(e->sh[i]), xev[i]));
+    }
+    first = ncclGroupStart();
     for (int i = 0; i < n && first == ncclSuccess; ++i) {
         gol_shard &s = e->sh[i];
         uint32_t *mid = s.bits[c];
@@ -710,7 +757,9 @@ static int step_launch(gol_engine *e, gol_shard &s, hipStream_t st, int k, int64
 }
 
 // Timing of one shard-step: events on the compute stream from the step's start to its end
-// (the edge stream joined).  The pool is folded into running sums when it is full.
+// (the edge stream joined).  The pool is folded into running sums when it is full -- only between
+// stepping calls (timing_begin): a call still open holds its start event and its exchanges' events,
+// unrecorded or unfolded, so within a call the pool grows instead.
 static int fold_timing(gol_engine *e)
 {
     for (const auto &t : e->timed) {
@@ -720,7 +769,10 @@ static int fold_timing(gol_engine *e)
         float x = 0;
         HIPCHK(hipEventElapsedTime(&x, s.tev[t.ev], s.tev[t.ev + 1]));
         if (t.exchange) {
+            float w = 0;
+            HIPCHK(hipEventElapsedTime(&w, s.tev[t.ev + 2], s.tev[t.ev + 3]));
             e->x_ms += x;
+            e->x_wait_ms += w;
             e->x_n += 1;
             continue;
         }
@@ -733,16 +785,16 @@ static int fold_timing(gol_engine *e)
     return GOL_OK;
 }
 
-static int timing_event(gol_engine *e, gol_shard &s, size_t *ev)
+// n consecutive events of shard s's pool (never folds: see fold_timing).
+static int timing_event(gol_shard &s, size_t *ev, size_t n = 2)
 {
-    if (s.tused + 2 > GOL_TIMING_EVENTS) RCCHK(fold_timing(e));
-    while (s.tused + 2 > s.tev.size()) {
+    while (s.tused + n > s.tev.size()) {
         hipEvent_t x;
         HIPCHK(hipEventCreate(&x));
         s.tev.push_back(x);
     }
     *ev = s.tused;
-    s.tused += 2;
+    s.tused += n;
     return GOL_OK;
 }
 
@@ -752,13 +804,16 @@ static int timing_event(gol_engine *e, gol_shard &s, size_t *ev)
 static int timing_begin(gol_engine *e)
 {
     if (!e->timing) return GOL_OK;
+    bool full = false;
+    for (const auto &s : e->sh) full |= s.tused + 2 > GOL_TIMING_EVENTS;
+    if (full) RCCHK(fold_timing(e));  // (no call is open here)
     e->tcall_ev.assign(e->sh.size(), 0);
     e->tcall_cells.assign(e->sh.size(), 0.0);
     e->tcall_steps = 0;
     for (size_t i = 0; i < e->sh.size(); ++i) {
         gol_shard &s = e->sh[i];
         RCCHK(set_dev(s.device));
-        RCCHK(timing_event(e, s, &e->tcall_ev[i]));
+        RCCHK(timing_event(s, &e->tcall_ev[i]));
         HIPCHK(hipEventRecord(s.tev[e->tcall_ev[i]], s.stream));
     }
     return GOL_OK;
@@ -768,14 +823,25 @@ static int timing_begin(gol_engine *e)
 // (gol_engine_step_flips) are not.
 static bool timing_open(const gol_engine *e) { return e->timing && e->tcall_ev.size() == e->sh.size(); }
 
-// GOL_TIMING_EXCHANGE: an event pair around one shard's part of a halo exchange on stream st
-// (xstart before the exchange's first operation on st, xstop after its last).
+// GOL_TIMING_EXCHANGE: four events around one shard's part of a halo exchange on stream st --
+// xtime_start before the exchange's first operation on st, xtime_wait / xtime_waited around the
+// part that waits for the neighbours (gol_engine_exchange_split), xtime_stop after its last.
 static int xtime_start(gol_engine *e, gol_shard &s, hipStream_t st, size_t *ev)
 {
     *ev = SIZE_MAX;
     if (!e->timing_x || !timing_open(e)) return GOL_OK;
-    RCCHK(timing_event(e, s, ev));
+    RCCHK(timing_event(s, ev, 4));
     HIPCHK(hipEventRecord(s.tev[*ev], st));
+    return GOL_OK;
+}
+static int xtime_wait(gol_shard &s, hipStream_t st, size_t ev)
+{
+    if (ev != SIZE_MAX) HIPCHK(hipEventRecord(s.tev[ev + 2], st));
+    return GOL_OK;
+}
+static int xtime_waited(gol_shard &s, hipStream_t st, size_t ev)
+{
+    if (ev != SIZE_MAX) HIPCHK(hipEventRecord(s.tev[ev + 3], st));
     return GOL_OK;
 }
 static int xtime_stop(gol_engine *e, gol_shard &s, hipStream_t st, size_t ev, int shard)
@@ -1711,8 +1777,11 @@ extern "C" int gol_engine_info(gol_engine *e, int32_t *k, int32_t *cells_per_lan
     const bool bits = e->mode == GOL_MODE_BITS;
     const bool band = bits && e->band_capable;
     const int dw = band ? e->band_dw : e->dw;
-    const bool pipe32 = e->mode == GOL_MODE_BYTES && e->k >= 32 && e->H >= 32 && e->W % 32 == 0;  // (advance)
-    const int kk = pipe32 ? 32 : pick_k(e->k, e->k, e->min_rows, dw, band);
+    // the k of the next launch, as advance() picks it
+    int kk = 1;  // the exact one-turn kernel: a board before its exact first turn, a byte board of W % 32 != 0 or non-0/255 bytes
+    if (bits) kk = pick_k(e->k, e->k, e->min_rows, dw, band);
+    else if (e->mode == GOL_MODE_BYTES && e->bytes_binary && e->W % 32 == 0)
+        kk = e->k >= 32 && e->H >= 32 ? 32 : pick_k(e->k, e->k, e->H, 1, false);
     if (k) *k = kk;
     if (cells_per_lane) *cells_per_lane = 32 * dw;
     if (strip_rows) {
@@ -1748,7 +1817,7 @@ extern "C" int gol_engine_set_timing(gol_engine *e, int32_t enable)
     for (auto &s : e->sh) s.tused = 0;
     e->t_ms = e->t_cells = 0;
     e->t_n = 0;
-    e->x_ms = 0;
+    e->x_ms = e->x_wait_ms = 0;
     e->x_n = 0;
     return GOL_OK;
 }
@@ -1757,9 +1826,21 @@ extern "C" int gol_engine_set_timing(gol_engine *e, int32_t enable)
 extern "C" int gol_engine_exchange_timing(gol_engine *e, int64_t *exchanges, double *mean_ms)
 {
     if (!e || !exchanges || !mean_ms) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (timing_open(e)) return gol_set_error(GOL_ESTATE, "a timed stepping call is in progress");
     RCCHK(fold_timing(e));
     *exchanges = e->x_n;
     *mean_ms = e->x_n ? e->x_ms / e->x_n : 0.0;
+    return GOL_OK;
+}
+
+extern "C" int gol_engine_exchange_split(gol_engine *e, int64_t *exchanges, double *mean_wait_ms, double *mean_transfer_ms)
+{
+    if (!e || !exchanges || !mean_wait_ms || !mean_transfer_ms) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (timing_open(e)) return gol_set_error(GOL_ESTATE, "a timed stepping call is in progress");
+    RCCHK(fold_timing(e));
+    *exchanges = e->x_n;
+    *mean_wait_ms = e->x_n ? e->x_wait_ms / e->x_n : 0.0;
+    *mean_transfer_ms = e->x_n ? (e->x_ms - e->x_wait_ms) / e->x_n : 0.0;
     return GOL_OK;
 }
 
@@ -1767,6 +1848,7 @@ extern "C" int gol_engine_exchange_timing(gol_engine *e, int64_t *exchanges, dou
 extern "C" int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double *mean_cell_updates)
 {
     if (!e || !launches || !mean_ms || !mean_cell_updates) return gol_set_error(GOL_EINVAL, "bad arguments");
+    if (timing_open(e)) return gol_set_error(GOL_ESTATE, "a timed stepping call is in progress");
     RCCHK(fold_timing(e));
     const int64_t n = e->t_n;
     *launches = n;

@@ -34,7 +34,8 @@ class gol_ipc;
 #define GOL_COLL_WORDS 16
 #define GOL_HOST_WORDS 16
 
-// Timing events per shard before the recorded steps are folded into running sums.
+// Timing events per shard before the recorded steps are folded into running sums (at the start
+// of a timed stepping call; within one call the pool grows instead, gol_engine.cpp timing_event).
 #define GOL_TIMING_EVENTS 512
 
 // One row shard: rows [y0, y1) of the board on one GPU.
@@ -82,7 +83,8 @@ struct gol_timed {
     size_t ev;  // index of the start event in the shard's pool (stop = ev + 1)
     double cell_updates;
     int64_t steps;  // k-turn steps between the two events
-    bool exchange = false;  // an event pair around one halo exchange (GOL_TIMING_EXCHANGE), not a stepping call
+    bool exchange = false;  // events around one halo exchange (GOL_TIMING_EXCHANGE), not a stepping call:
+                            // ev, ev + 1 the whole exchange, ev + 2 .. ev + 3 its wait for the neighbours
 };
 
 struct gol_engine {
@@ -125,7 +127,7 @@ struct gol_engine {
     int64_t tcall_steps = 0;           // and its k-turn steps
     double t_ms = 0, t_cells = 0;  // folded timing sums (timed pool recycled)
     int64_t t_n = 0;
-    double x_ms = 0;               // folded exchange timing sums
+    double x_ms = 0, x_wait_ms = 0;  // folded exchange timing sums (whole exchange, wait for the neighbours)
     int64_t x_n = 0;
 };
 

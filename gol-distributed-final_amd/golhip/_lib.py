@@ -128,6 +128,7 @@ SIGNATURES = [
     ("gol_engine_set_timing", ctypes.c_int, [_vp, _i32]),
     ("gol_engine_timing", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double), _P(ctypes.c_double)]),
     ("gol_engine_exchange_timing", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double)]),
+    ("gol_engine_exchange_split", ctypes.c_int, [_vp, _P(_i64), _P(ctypes.c_double), _P(ctypes.c_double)]),
     ("gol_halo_plan", ctypes.c_int, [_i64, _i32, _i32, _i32, _P(gol_halo_op), _i32, _P(_i32)]),
     ("gol_step_plan", ctypes.c_int, [_i64, _i32, _i32, _i32, _P(gol_launch), _i32, _P(_i32)]),
     ("gol_dev_bits_step", ctypes.c_int,

@@ -230,10 +230,13 @@ class Engine:
         self._check(self._L.gol_engine_set_timing(self._h, level))
 
     def exchange_timing(self) -> dict:
-        """Halo exchanges timed since set_timing(True, exchanges=True) and their mean duration."""
-        n, ms = ctypes.c_int64(), ctypes.c_double()
+        """Halo exchanges timed since set_timing(True, exchanges=True): their mean duration, and
+        its split (gol_engine_exchange_split) into the wait for the ring neighbours to reach the
+        exchange and the transfer of the halo rows."""
+        n, ms, w, x = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         self._check(self._L.gol_engine_exchange_timing(self._h, ctypes.byref(n), ctypes.byref(ms)))
-        return {"exchanges": n.value, "mean_ms": ms.value}
+        self._check(self._L.gol_engine_exchange_split(self._h, ctypes.byref(n), ctypes.byref(w), ctypes.byref(x)))
+        return {"exchanges": n.value, "mean_ms": ms.value, "wait_ms": w.value, "transfer_ms": x.value}
 
     def timing(self) -> dict:
         """HIP-event timing of every shard-step since set_timing(True) (edge launches included)."""

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GOL_ABI_VERSION 5
+#define GOL_ABI_VERSION 6
 
 enum {
     GOL_OK = 0,
@@ -256,6 +256,14 @@ int gol_engine_timing(gol_engine *e, int64_t *launches, double *mean_ms, double 
  * nothing (0). */
 #define GOL_TIMING_EXCHANGE 2
 int gol_engine_exchange_timing(gol_engine *e, int64_t *exchanges, double *mean_ms);
+/* ABI 6: the same exchanges split in two.  mean_wait_ms is the part spent
+ * waiting for the ring neighbours to reach the exchange: the IPC transport's
+ * poll of their READY flags; on RCCL a one-word send/recv with each neighbour
+ * issued first (only while exchanges are timed), whose completion means every
+ * neighbour has posted its side.  mean_transfer_ms is the rest (the halo rows
+ * themselves once both sides are there).  Transports without peers in other
+ * processes (LOCAL, LOOPBACK) wait for nothing on the exchange's stream: 0. */
+int gol_engine_exchange_split(gol_engine *e, int64_t *exchanges, double *mean_wait_ms, double *mean_transfer_ms);
 
 /* ---------------------------------------------------------------- plans
  * The schedule of a sharded step as data (host functions, no GPU needed).  The

@@ -58,7 +58,7 @@ def test_header_compiles(tmp_path, compiler, lang):
 
 
 def test_abi_version(G):
-    assert G.lib().gol_abi_version() == 5
+    assert G.lib().gol_abi_version() == 6
 
 
 def test_ipc_unique_id_host_only(G):

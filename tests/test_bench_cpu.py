@@ -32,6 +32,9 @@ def test_self_launch_two_ranks_dry_run():
     rs = d["config"]["rank_stats"]
     assert rs["launch_ms"] == {"max": 0.5, "min": 0.25}
     assert rs["exchange_ms"] == {"max": 0.02, "min": 0.01}
+    # its split: the wait for the ring neighbours and the transfer (gol_engine_exchange_split)
+    assert rs["exchange_wait_ms"] == {"max": 0.008, "min": 0.004}
+    assert rs["exchange_transfer_ms"] == {"max": 0.012, "min": 0.006}
     assert rs["wall_ms"] == {"max": 2.0, "min": 1.0}
     assert rs["nranks_seen"] == [2, 2] and rs["exchanges_per_rank"] == [20, 20]  # (the warmup's: weak's default 20)
     assert rs["transports"] == ["dry-run"] and "basis" in rs
@@ -76,3 +79,71 @@ def test_roofline_uses_only_current_profiles(tmp_path, monkeypatch):
     assert stale is None and why.startswith("stale")
     r = bench.roofline("bits", 12.0, 1e12, None, "missing")
     assert r["bound"] == "hbm" and r["frac"] is None and r["traffic"] is None
+
+
+class _OneRank:
+    world, rank = 1, 0
+
+    def gather(self, obj):
+        return [obj]
+
+
+def test_parity_check_against_reference_series(tmp_path, monkeypatch):
+    """bench.parity: every count of the run against the reference series of its board; a
+    mismatch names the first turn that differs, a run longer than the series is 'partial', a
+    board without a series 'unpinned'."""
+    fx = tmp_path / "counts.json"
+    fx.write_text(json.dumps({"boards": {"8x64": {"every": 4, "counts": [10, 11, 12, 13]}}}))
+    monkeypatch.setattr(bench, "COUNTS_FIXTURE", str(fx))
+    r = _OneRank()
+    assert bench.parity(r, "8x64", 4, [10, 11, 12])["status"] == "ok"
+    bad = bench.parity(r, "8x64", 4, [10, 11, 99, 13])
+    assert bad["status"] == "FAIL" and bad["turn"] == 12 and bad["got"] == 99 and bad["want"] == 12
+    assert bench.parity(r, "8x64", 4, [10, 11, 12, 13, 14])["status"] == "partial"
+    assert bench.parity(r, "8x64", 8, [11])["status"] == "unpinned"
+    assert bench.parity(r, "16x64", 4, [1])["status"] == "unpinned"
+
+
+def _fixture():
+    with open(bench.COUNTS_FIXTURE) as f:
+        return json.load(f)["boards"]
+
+
+def test_reference_series_cover_the_bench_runs():
+    """tests/golden/bench_counts.json holds a series for every board bench.py times -- the weak
+    board at 1/2/4/8 ranks (the driver's SCALE runs), 262144^2 at any rank count, 65536^2 and the
+    byte board -- long enough for the default runs and the driver's --steps 20 --warmup 5."""
+    boards = _fixture()
+
+    def need(workload, world, steps, warmup):
+        a = bench.parse(["--workload", workload, "--gpus", str(world)] +
+                        (["--steps", str(steps), "--warmup", str(warmup)] if steps else []))
+        if workload == "byte16k":
+            H = W = 16384
+            k, rate, per_rank = 32, bench.SETTLE_RATE_BYTES, H * W
+        else:
+            H, W = {"weak": (a.rows_per_gpu * world, a.width), "strong262k": (262144, 262144),
+                    "bit64k": (65536, 65536)}[workload]
+            k, rate = 12, bench.SETTLE_RATE_BITS
+            per_rank = (H // world if workload in ("weak", "strong262k") else H) * W
+        settle = bench.settle_steps(a, lambda n: None, float(per_rank) * k, rate)
+        return f"{H}x{W}", k, settle + a.warmup + a.steps
+
+    for workload, worlds in (("weak", (1, 2, 4, 8)), ("strong262k", (1, 2, 4, 8)), ("bit64k", (1,)), ("byte16k", (1,))):
+        for world in worlds:
+            for steps, warmup in ((None, None), (20, 5)):
+                key, k, points = need(workload, world, steps, warmup)
+                assert key in boards, key
+                assert boards[key]["every"] == k and len(boards[key]["counts"]) >= points, (key, points)
+
+
+def test_reference_series_start_as_the_oracle():
+    """The first points of two series against the oracle's word-parallel run of the same
+    load_random(1) board (the rest: tiled-oracle GPU tests pin the kernels that made them)."""
+    from oracle import oracle as O
+    boards = _fixture()
+    for key, H, W, turns in (("16384x16384", 16384, 16384, 32), ("4096x65536", 4096, 65536, 24)):
+        s = boards[key]
+        _, rc = O.bits_run(O.random_words(1, 0, H, W // 64), turns, with_counts=True)
+        e = s["every"]
+        assert s["counts"][:turns // e] == [int(rc[e * (i + 1) - 1]) for i in range(turns // e)]

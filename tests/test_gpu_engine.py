@@ -534,6 +534,46 @@ def test_bytes_layout_engine(golhip, shape):
             e.hash()
 
 
+def test_byte16k_engine_full_size(golhip):
+    """Config 2's engine path at its size: Engine(16384, 16384, layout="bytes"),
+    load_random(1), two counted k = 32 launches of the byte pipeline -- the path bench.py's byte16k
+    line times -- against the bit oracle's 64 turns: the board and both fused counts."""
+    H = W = 16384
+    with golhip.Engine(H, W, device=0, layout="bytes") as e:
+        assert e.info()["turns_per_launch"] == 32 and e.info()["layout"] == "bytes"
+        e.load_random(1)
+        counts = e.step_counted(64, 32)
+        got = e.store_bytes()
+    ref, rc = O.bits_run(O.random_words(1, 0, H, W // 64), 64, with_counts=True)
+    assert counts.tolist() == [int(rc[31]), int(rc[63])]
+    assert np.array_equal(got, O.unpack(ref))
+
+
+def test_default_k_on_w32_byte_board(golhip):
+    """a board of W % 64 == 32 is a byte board whatever the layout, and its default k
+    is the byte pipeline's 32 (round 5 changed it from 8): 203 x 32*67 at the default k -- two
+    counted k = 32 launches and a 5-turn tail of the blocked kernel -- against the literal port;
+    the info call reports what the next launch runs (1 before the exact first turn of non-0/255
+    bytes)."""
+    H, W = 203, 32 * 67
+    rng = np.random.default_rng(67)
+    board = (rng.random((H, W)) < 0.4).astype(np.uint8) * 255
+    with golhip.Engine(H, W, device=0) as e:
+        assert e.info()["layout"] == "bytes" and e.info()["turns_per_launch"] == 32
+        e.load_bytes(board)
+        counts = e.step_counted(64, 32)
+        e.step(5)
+        got = e.store_bytes()
+        odd = board.copy()
+        odd[0, 0] = 7
+        e.load_bytes(odd)
+        assert e.info()["turns_per_launch"] == 1
+    mid = O.run(board, 32, 4)
+    end = O.run(mid, 32, 4)
+    assert counts.tolist() == [int(np.count_nonzero(mid)), int(np.count_nonzero(end))]
+    assert np.array_equal(got, O.run(end, 5, 4))
+
+
 def test_bytes_layout_timing_and_rank_refusal(golhip):
     """The byte board's launches are timed like the bit board's (bench.py byte16k reads them), and
     a byte board does not shard."""

@@ -237,4 +237,42 @@ def test_bench_share_gpu_shards_over_ipc(G):
     assert n[0] == n[1] and 1 <= n[0] <= 2, n
     assert 0 < rs["launch_ms"]["min"] <= rs["launch_ms"]["max"]
     assert 0 < rs["exchange_ms"]["min"] <= rs["exchange_ms"]["max"]  # (the warmup's: incl. the first exchange)
+    # its split (gol_engine_exchange_split): the IPC READY polls and the rest
+    assert 0 <= rs["exchange_wait_ms"]["min"] <= rs["exchange_wait_ms"]["max"] <= rs["exchange_ms"]["max"]
+    assert 0 < rs["exchange_transfer_ms"]["min"] <= rs["exchange_transfer_ms"]["max"]
     assert "rank_stats" not in one["config"]
+    # every count of both runs against the reference series of the 4096 x 65536 board
+    for d in (one, two):
+        assert d["config"]["parity"]["status"] == "ok", d["config"]["parity"]
+    assert two["config"]["parity"]["ranks"] == ["ok", "ok"]
+
+
+def _bench(args, timeout=300):
+    p = subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr[-3000:]
+
+
+def test_bench_share_gpu_weak_board_parity(G):
+    """The weak workload as the driver's N = 2 run sizes it (2 x 2^17 rows x 2^20, the default
+    settle steps), 2 rank processes on this GPU over IPC: every alive count of the run equals one
+    GPU's series of the same 2^18 x 2^20 torus (tests/golden/bench_counts.json)."""
+    rc, d, err = _bench(["--gpus", "2", "--share-gpu", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
+    assert rc == 0 and d, err
+    assert d["config"]["H"] == 1 << 18 and d["config"]["parallelism"] == "rows2"
+    par = d["config"]["parity"]
+    assert par["status"] == "ok" and par["turns_checked"] == d["config"]["turns_done"], par
+
+
+def test_bench_mispaired_halo_fails_the_line(G):
+    """A build whose ranks put each received halo block in the wrong ghost rows
+    (libgolhip_mispair.so, GOL_TEST_MISPAIR) computes a plausible but wrong torus: bench.py's
+    parity check names the first turn whose count differs and the run exits nonzero."""
+    lib = os.path.join(ROOT, "gol-distributed-final_amd", "golhip", "libgolhip_mispair.so")
+    if not os.path.exists(lib):
+        pytest.skip("libgolhip_mispair.so not built (make -C gol-distributed-final_amd/csrc mispair)")
+    rc, d, err = _bench(["--gpus", "2", "--share-gpu", "--rows-per-gpu", "2048", "--width", "65536", "--steps", "3",
+                         "--warmup", "1", "--no-cpu-baseline", "--settle-s", "0", "--library", lib])
+    assert rc == 1 and d, err
+    par = d["config"]["parity"]
+    assert par["status"] == "FAIL" and par["turn"] == 12 and par["got"] != par["want"], par

@@ -325,6 +325,36 @@ def test_timing_counts_the_step_launches(G):
         assert t["mean_cell_updates"] == 300 * 2048 * 12
 
 
+def test_timing_many_exchanges_in_one_call(G):
+    """one timed call with more exchanges than the event pool holds (2 loopback shards,
+    300 exchanges of 4 events per shard against a pool of 512).  The pool grows inside the call
+    instead of being folded while the call's own start event is live, so the call's step time is
+    the same as with exchange timing off, every exchange is counted, and the loopback exchange
+    (no peer in another process) waits for nothing.  The board is the oracle's either way."""
+    H, W, k, steps = 64, 1024, 4, 300
+    res = {}
+    for x in (False, True):
+        with _sharded(G, H, W, 2, turns_per_launch=k) as e:
+            e.load_random(4)
+            e.step(12 * k)  # (clocks, allocations)
+            e.set_timing(True, exchanges=x)
+            e.step(steps * k)
+            t, xt = e.timing(), e.exchange_timing()
+            e.set_timing(False)
+            res[x] = (t, xt, e.hash())
+    ref = O.bits_run(O.random_words(4, 0, H, W // 64), (12 + steps) * k)
+    for t, xt, h in res.values():
+        assert h == O.hash_words(ref)
+        assert t["launches"] == 2 * steps and t["mean_cell_updates"] == 32 * W * k
+    t0, x0, _ = res[False]
+    t1, x1, _ = res[True]
+    assert x0["exchanges"] == 0
+    assert x1["exchanges"] >= 2 * steps and x1["mean_ms"] > 0
+    # (two events recorded back to back on a stream still read ~10 us apart)
+    assert 0 <= x1["wait_ms"] < 0.05 and abs(x1["wait_ms"] + x1["transfer_ms"] - x1["mean_ms"]) < 1e-9
+    assert 0.5 < t1["mean_ms"] / t0["mean_ms"] < 2.0, (t0, t1)
+
+
 def test_timing_then_flips_outside_a_timed_call(G):
     """with timing on, a step_flips call (not a timed stepping call) must not write the
     per-call timing arrays (it used to index them out of bounds when no step had run) and must not

@@ -50,7 +50,7 @@ import golhip as G
 from golhip._lib import gol_config, gol_request, gol_response, lib
 from oracle import oracle as O
 
-assert lib().gol_abi_version() == 5
+assert lib().gol_abi_version() == 6
 for H in (0, 1, 2, 10, 17, 512, 1 << 20):
     for T in (1, 2, 3, 7, 16):
         for i in range(T):
