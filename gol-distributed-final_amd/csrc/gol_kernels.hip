@@ -1007,22 +1007,46 @@ band_pipe_kernel(BitsArgs a)
     const __amdgpu_buffer_rsrc_t strip_rs = __builtin_amdgcn_make_buffer_rsrc(
         dst_b + (int64_t)s0 * pitch_b, (short)0, (int)(nrows * (uint32_t)pitch_b), 0x00020000);
     // (walking up, dir -1: output row y = s1e - 1 + 2K - 2b - S, offsets decreasing)
-    int rrel = dir >= 0 ? -2 * K : s1e - 1 + 2 * K - s0;  // output row - s0 (wave-uniform)
+    // (readfirstlane: the compiler otherwise keeps this uniform row index in a VGPR and compares it
+    // with a vector compare per row)
+    int rrel = __builtin_amdgcn_readfirstlane(dir >= 0 ? -2 * K : s1e - 1 + 2 * K - s0);  // output row - s0
     const int rstep = dir >= 0 ? 1 : -1;
     uint32_t voff = st_off + (uint32_t)rrel * (uint32_t)pitch_b;
     const uint32_t vstep = (uint32_t)rstep * (uint32_t)pitch_b;
-    auto emit = [&](const uint32_t (&cur)[DW]) {
-        __builtin_amdgcn_raw_buffer_store_b128(pack(cur), strip_rs, voff, 0, GOL_BAND_STORE_AUX);
-        // fused count of the rows this strip stores: a v_bcnt chain that accumulates, kept only
-        // for the strip's rows (a uniform select; halo lanes are masked once at the end)
-        // (written as a chain, compiled to v_bcnt pairs + v_add3 + a select: forcing the chain with
-        // inline asm costs an s_nop after each asm statement, the hazard recognizer cannot see in)
+    // a row's cells onto the count: one accumulating v_bcnt per word, as one asm statement (the
+    // compiler turns the same chain in C into bcnt pairs + v_add3).  Plain VALU reading VALU
+    // results: no wait states inside (tools/check_lds_wait.py checks the pipeline kernels' asm for
+    // the VALU hazards the compiler cannot see).
+    auto count_row = [&](const uint32_t (&cur)[DW]) {
+        uint32_t c = 0;
+        asm("v_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0\n\tv_bcnt_u32_b32 %0, %3, %0\n\t"
+            "v_bcnt_u32_b32 %0, %4, %0"
+            : "=&v"(c)
+            : "v"(cur[0]), "v"(cur[1]), "v"(cur[2]), "v"(cur[3]));
+        return c;
+    };
+    auto count_rows2 = [&](const uint32_t (&x0)[DW], const uint32_t (&x1)[DW]) {
+        asm("v_bcnt_u32_b32 %0, %1, %0\n\tv_bcnt_u32_b32 %0, %2, %0\n\tv_bcnt_u32_b32 %0, %3, %0\n\t"
+            "v_bcnt_u32_b32 %0, %4, %0\n\tv_bcnt_u32_b32 %0, %5, %0\n\tv_bcnt_u32_b32 %0, %6, %0\n\t"
+            "v_bcnt_u32_b32 %0, %7, %0\n\tv_bcnt_u32_b32 %0, %8, %0"
+            : "+v"(alive)
+            : "v"(x0[0]), "v"(x0[1]), "v"(x0[2]), "v"(x0[3]), "v"(x1[0]), "v"(x1[1]), "v"(x1[2]), "v"(x1[3]));
+    };
+    // the block's two output rows to HBM, and the fused count of the rows this strip stores (halo
+    // lanes are masked once at the end): one v_bcnt chain of 8 words onto the count, and a block at
+    // a strip's end (a row outside it: a uniform branch) takes the count of that row off again.
+    // (Round 5's per-row select cost 15 VALU per block instead of 8: the count in bcnt pairs +
+    // v_add3, a vector compare and a select per row.)
+    auto emit2 = [&](const uint32_t (&x0)[DW], const uint32_t (&x1)[DW]) {
+        __builtin_amdgcn_raw_buffer_store_b128(pack(x0), strip_rs, voff, 0, GOL_BAND_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(pack(x1), strip_rs, voff + vstep, 0, GOL_BAND_STORE_AUX);
         if constexpr (COUNT) {
-            const uint32_t c = __popc(cur[3]) + (__popc(cur[2]) + (__popc(cur[1]) + (__popc(cur[0]) + alive)));
-            alive = (uint32_t)rrel < nrows ? c : alive;
+            count_rows2(x0, x1);
+            const bool in0 = (uint32_t)rrel < nrows, in1 = (uint32_t)(rrel + rstep) < nrows;  // wave-uniform
+            if (!(in0 && in1)) alive -= (in0 ? 0u : count_row(x0)) + (in1 ? 0u : count_row(x1));
         }
-        voff += vstep;
-        rrel += rstep;
+        voff += 2 * vstep;
+        rrel += 2 * rstep;
     };
     lds_u32 *const src_base = wv == 0 ? in_base : rd_base;
     // paired: the loader's claims, NS blocks (one loop trip) each, one in flight (issued at a
@@ -1085,8 +1109,7 @@ band_pipe_kernel(BitsArgs a)
             for (int g = 0; g < KW; ++g) pstage<DW>(st[g], r0, r1);
         }
         if constexpr (LAST) {
-            emit(r0);
-            emit(r1);
+            emit2(r0, r1);
         } else {
             if (seen_free < b + 1 - NS) {  // slot b % NS: block b - NS consumed
                 seen_free = spin_until_ge(consumed_l + wv + 1, b + 1 - NS);

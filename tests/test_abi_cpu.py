@@ -7,6 +7,7 @@
   error codes instead of crashes, PGM codec, wire names of stubs.go.
 """
 import os
+import sys
 import re
 import subprocess
 
@@ -179,6 +180,32 @@ def test_pipe_kernels_wait_before_reading_lds(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "0 hazards" in r.stdout
+
+
+def test_valu_hazard_checker_catches_asm_hazards():
+    """tools/check_lds_wait.py's VALU-hazard scan (round 6) on hand-made assembly: a v_dot4 result
+    read at once, a DPP move of a register an asm VALU just wrote, an asm LDS DMA right after an
+    M0 write -- and the same sequences padded with s_nop, or produced by compiler code (which
+    hipcc pads itself), pass."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_lds_wait as C
+
+    def scan(text):
+        return C.valu_hazards(text)
+    bad_dot = ";;#ASMSTART\n\tv_dot4_i32_i8 v1, v2, v3, v4\n;;#ASMEND\n\tv_add_u32_e32 v5, v1, v6\n"
+    assert len(scan(bad_dot)) == 1
+    assert not scan(bad_dot.replace(";;#ASMEND", "\ts_nop 2\n;;#ASMEND"))
+    bad_dpp = (";;#ASMSTART\n\tv_bcnt_u32_b32 v7, v8, v7\n;;#ASMEND\n"
+               "\tv_mov_b32_dpp v9, v7 wave_shr:1 row_mask:0xf bank_mask:0xf\n")
+    assert len(scan(bad_dpp)) == 1
+    assert not scan(bad_dpp.replace(";;#ASMEND\n", ";;#ASMEND\n\ts_nop 1\n"))
+    assert not scan(bad_dpp.replace(";;#ASMSTART\n", "").replace(";;#ASMEND\n", ""))  # hipcc's own: padded by it
+    bad_m0 = ";;#ASMSTART\n\ts_mov_b32 m0, s4\n\tglobal_load_lds_dwordx4 v[2:3], off\n;;#ASMEND\n"
+    assert len(scan(bad_m0)) == 1
+    assert not scan(bad_m0.replace("\tglobal_load", "\ts_nop 0\n\tglobal_load"))
+    fall = "\tv_bcnt_u32_b32 v7, v8, v7\n.LBB0_1:\n;;#ASMSTART\n\tv_mov_b32_dpp v9, v7 row_shr:1\n;;#ASMEND\n"
+    assert len(scan(fall)) == 1  # a label is also a fall-through
+    assert not scan(fall.replace(".LBB0_1:", "\ts_branch .LBB0_2\n.LBB0_1:"))
 
 
 def test_go_shims_use_only_declared_c_symbols():

@@ -1,4 +1,5 @@
-"""Check the split-issue LDS reads of the pipeline kernels in the gfx950 assembly.
+"""Check the split-issue LDS reads and the inline-asm VALU hazards of the pipeline kernels in the
+gfx950 assembly.
 
 The pipe kernels issue ds_read from inline asm and wait for it in a later asm
 statement (lds_*_issue / lds_wait*), so the compiler does not see the read as
@@ -113,6 +114,85 @@ def check(body):
     return hazards
 
 
+# VALU hazards the compiler cannot see (round 6): hipcc pads the wait states of the
+# instructions it emits itself, but not those whose producer or consumer sits inside an inline-asm
+# statement (cdna_hip_programming.md §5.7 item 2).  Rules checked, as (consumer, states after a
+# VALU write of the register it reads):
+#   DPP source (v_mov_b32_dpp ... row_/wave_ controls)     2   (VALU write VGPR -> DPP read)
+#   v_readfirstlane / v_readlane source VGPR               1
+#   v_permlane16/32_swap either operand                    2
+#   any VALU source after a v_dot* result                  3   (the round-5 stale-sum bug)
+#   global_load_lds / buffer_load ... lds after an M0 write 1  (SALU write M0 -> LDS DMA)
+# Wait states: every instruction between producer and consumer counts 1, s_nop N counts N + 1.
+# The scan is straight-line (fall-through across labels; an unconditional branch resets it); it reports
+# only pairs with an end inside an ASMSTART/ASMEND region -- the compiler pads the rest.
+HAZARD_RULES = (
+    ("dpp", 2), ("readlane", 1), ("permlane", 2), ("dot", 3),
+)
+
+
+def _dsts_srcs(op, rest):
+    dst, _, src = rest.partition(",")
+    return regs(dst), regs(src)
+
+
+def valu_hazards(body):
+    out = []
+    last_write = {}   # vgpr -> (instruction position in wait states, producer kind, in_asm)
+    m0_write = None   # position of the last M0 write
+    pos = 0
+    in_asm = False
+    for i, line in enumerate(body.splitlines()):
+        t = line.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        s = line.split(";")[0].strip()
+        if not s or s.startswith(".") or s.endswith(":"):
+            continue  # (labels: a fall-through keeps the state -- conservative)
+        op, _, rest = s.partition(" ")
+        if op in ("s_branch", "s_setpc_b64"):
+            last_write.clear()  # the next instruction is reached only by a branch
+            m0_write = None
+            continue
+        if op == "s_nop":
+            pos += int(rest.strip() or "0", 0) + 1
+            continue
+        pos += 1
+        if op.startswith("v_"):
+            dsts, srcs = _dsts_srcs(op, rest)
+            dpp = "_dpp" in op or re.search(r"\b(row_|wave_|quad_perm|row_bcast)", rest)
+            kinds = []
+            if dpp:
+                kinds.append(("dpp", 2))
+            if op.startswith(("v_readfirstlane", "v_readlane")):
+                kinds.append(("readlane", 1))
+            if op.startswith("v_permlane"):
+                kinds.append(("permlane", 2))
+                srcs = srcs | dsts
+            for r in srcs:
+                w = last_write.get(r)
+                if not w:
+                    continue
+                wpos, wkind, wasm = w
+                need = max([n for _, n in kinds] + ([3] if wkind == "dot" else []) + [0])
+                if need and pos - wpos - 1 < need and (wasm or in_asm):
+                    out.append((i, s, f"v{r} written {pos - wpos - 1} wait states before, needs {need}"))
+            kind = "dot" if op.startswith("v_dot") else "valu"
+            for r in dsts:
+                last_write[r] = (pos, kind, in_asm)
+        elif op.startswith("s_") and re.match(r"\s*m0\b", rest):
+            m0_write = (pos, in_asm)
+        elif (op.startswith("global_load_lds") or (op.startswith("buffer_load") and " lds" in rest)) and m0_write:
+            mpos, masm = m0_write
+            if pos - mpos - 1 < 1 and (masm or in_asm):
+                out.append((i, s, "M0 written 0 wait states before an LDS DMA, needs 1"))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("asm", nargs="?")
@@ -130,6 +210,9 @@ def main():
         for i, s, r in check(body):
             bad += 1
             print(f"{name}: line {i}: reads in-flight v{r}: {s}")
+        for i, s, why in valu_hazards(body):
+            bad += 1
+            print(f"{name}: line {i}: VALU hazard ({why}): {s}")
     # the pipeline kernels must not spill: scratch traffic inside the pipeline loop costs more
     # than the kernel's whole LDS hand-off (and reads in-flight registers, as above)
     for blk in re.findall(r"- \.agpr_count.*?(?=\n  - \.agpr_count|\namdhsa\.target)", asm, re.S):

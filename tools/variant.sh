@@ -7,6 +7,7 @@
 #                                               (environment BANDFLAGS / BYTEFLAGS / KFLAGS, if set,
 #                                               replace the Makefile's scheduler / kernel flags)
 #   tools/variant.sh rev REV NAME               every source (and golhip.h) of a git revision
+#   tools/variant.sh patch NAME FILE [FLAGS]    current sources with FILE (a patch of csrc/, -p1) applied
 #   tools/variant.sh kernels REV NAME           current sources with gol_kernels.hip of REV (the
 #                                               kernels of REV behind today's engine and ABI)
 #   tools/variant.sh res ["-DFLAG ..."]         VGPRs / LDS / scratch / occupancy of the pipe kernels
@@ -38,6 +39,14 @@ case ${1:-} in
     done
     git -C "$R" show "$REV:include/golhip.h" > "$D/include/golhip.h"
     make -s -j8 -C "$D/pkg/csrc" ARCH=gfx950 BUILD=./obj OUT="$V/lib$N.so" INC="$D/include"
+    rm -rf "$D"
+    echo "$V/lib$N.so" ;;
+  patch)  # current sources with a patch (tools/exp/*.patch, paths relative to csrc/) applied
+    N=$2; P=$3; D=$V/src_$N
+    copy_current "$D"
+    patch -s -d "$D" -p1 < "$R/$P"
+    make -s -j8 -C "$D" ARCH=gfx950 BUILD=./obj OUT=../lib$N.so INC=$R/include \
+        CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -I$R/include -I. ${4:-}"
     rm -rf "$D"
     echo "$V/lib$N.so" ;;
   kernels)
