@@ -12,6 +12,7 @@
 #                                           python tools/timeline.py build -DGOL_EXP_CLOCK --out libclock)
 #   tools/gpu.sh ab BASE "bench args;..."   same-box A/B of tools/variants/libBASE.so against the product
 #   tools/gpu.sh share                      the several-process (IPC) rank tests + --share-gpu bench lines
+#   tools/gpu.sh share_parity               the weak board at N = 2 and 4 rank processes on one GPU: parity
 #   tools/gpu.sh final TAG                  suite, profile TAG, clock (if built), bench: a round's evidence
 #   tools/gpu.sh driver                     the driver's bench command twice + once under rocprofv3 --stats
 #                                           (gpurun_out/drv/: bench_1/2.json, bench_trace.json, trace/)
@@ -85,6 +86,14 @@ share() {
   tail -4 gpurun_out/share.jsonl
 }
 
+share_parity() {  # the weak board as the driver's N = 2 and 4 runs size it, rank processes on this GPU (IPC)
+  export GOL_IPC_TIMEOUT_MS=60000
+  for n in 2 4; do
+    timeout -k 10 300 python3 -u bench.py --gpus $n --share-gpu --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/share_parity_$n.json 2> gpurun_out/share_parity_$n.err || { tail -5 gpurun_out/share_parity_$n.err; exit 8; }
+    python3 -c "import json; d=json.load(open('gpurun_out/share_parity_$n.json')); c=d['config']; print($n, d['value'], c['H'], c['parity']['status'], c['parity']['turns_checked'], c['rank_stats']['exchange_ms'], c['rank_stats']['exchange_wait_ms'])"
+  done
+}
+
 driver() {  # the round-end driver's own command (bench.py --gpus 1 --steps 20 --warmup 5)
   mkdir -p gpurun_out/drv
   for i in 1 2; do
@@ -105,6 +114,7 @@ case $cmd in
   clock) clock "$@" ;;
   ab) ab "$@" ;;
   share) share ;;
+  share_parity) share_parity ;;
   driver) driver ;;
   final)
     tag=${1:?tag}
