@@ -163,7 +163,16 @@ class Ranks:
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # gloo's C++ side prints "[Gloo] Rank r is connected to ..." on stdout: to stderr, so
+            # that rank 0's stdout holds nothing but the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
             assert dist.get_world_size() == args.gpus
             self.dist = dist
         self.dry = args.dry_run

@@ -17,8 +17,10 @@ def test_self_launch_two_ranks_dry_run():
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run", "--steps", "4"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1
+    # rank 0's stdout is the one JSON line and nothing else (gloo's "[Gloo] Rank 0 is connected"
+    # message goes to stderr): a driver may read the first line
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["ranks"] == 2
     # max over ranks: rank 1 reported 2 ms, rank 0 1 ms

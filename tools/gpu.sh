@@ -90,7 +90,7 @@ share_parity() {  # the weak board as the driver's N = 2 and 4 runs size it, ran
   export GOL_IPC_TIMEOUT_MS=60000
   for n in 2 4; do
     timeout -k 10 300 python3 -u bench.py --gpus $n --share-gpu --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/share_parity_$n.json 2> gpurun_out/share_parity_$n.err || { tail -5 gpurun_out/share_parity_$n.err; exit 8; }
-    python3 -c "import json; d=json.load(open('gpurun_out/share_parity_$n.json')); c=d['config']; print($n, d['value'], c['H'], c['parity']['status'], c['parity']['turns_checked'], c['rank_stats']['exchange_ms'], c['rank_stats']['exchange_wait_ms'])"
+    python3 -c "import json; ls=open('gpurun_out/share_parity_$n.json').read().splitlines(); assert len(ls) == 1, ls; d=json.loads(ls[0]); c=d['config']; print($n, d['value'], c['H'], c['parity']['status'], c['parity']['turns_checked'], c['rank_stats']['exchange_ms'], c['rank_stats']['exchange_wait_ms'])"
   done
 }
 
