@@ -249,6 +249,27 @@ def test_rccl_transport_self(G):
         assert np.array_equal(e.store_rows(10, 20), O.unpack(ref)[10:20])
 
 
+@pytest.mark.parametrize("step", ["serial", "overlap"])
+def test_rccl_exchange_timing_self(G, step):
+    """The timed RCCL exchange (ABI 6, what bench.py's N > 1 warmup runs on every rank): a one-word
+    send/recv with each ring neighbour ahead of the halo group, here a one-rank Engine.rank whose
+    neighbour is itself, on the compute stream after SERIAL steps and on the comm stream after
+    OVERLAP ones.  The board is the oracle's, every exchange is timed, and the wait and the
+    transfer add up to the whole."""
+    H, W, k = 1000, 2048, 12
+    ref, counts = O.bits_run(O.random_words(5, 0, H, W // 64), 60, with_counts=True)
+    with G.Engine.rank(H, W, 1, 0, G.engine.rccl_unique_id(), device=0, transport="rccl", step=step) as e:
+        e.load_random(5)
+        e.set_timing(True, exchanges=True)
+        got = e.step_counted(60, k)
+        x = e.exchange_timing()
+        e.set_timing(False)
+        assert got.tolist() == [int(counts[k * (i + 1) - 1]) for i in range(5)]
+        assert e.hash() == O.hash_words(ref)
+    assert x["exchanges"] >= 5 and x["mean_ms"] > 0
+    assert 0 <= x["wait_ms"] and 0 <= x["transfer_ms"] and abs(x["wait_ms"] + x["transfer_ms"] - x["mean_ms"]) < 1e-9
+
+
 def test_broker_run_sharded(G, golden_dir):
     """Operations.Run with the board sharded over 3 shards (Threads 1..16 as in TestGol): the
     same alive list and board as check/images; the 16x16 board (W % 64 != 0) runs unsharded."""
