@@ -812,9 +812,14 @@ static int timing_begin(gol_engine *e)
     e->tcall_steps = 0;
     for (size_t i = 0; i < e->sh.size(); ++i) {
         gol_shard &s = e->sh[i];
-        RCCHK(set_dev(s.device));
-        RCCHK(timing_event(s, &e->tcall_ev[i]));
-        HIPCHK(hipEventRecord(s.tev[e->tcall_ev[i]], s.stream));
+        int rc = set_dev(s.device);
+        if (rc == GOL_OK) rc = timing_event(s, &e->tcall_ev[i]);
+        if (rc == GOL_OK && hipEventRecord(s.tev[e->tcall_ev[i]], s.stream) != hipSuccess)
+            rc = gol_set_error(GOL_EHIP, "timing: hipEventRecord failed");
+        if (rc != GOL_OK) {
+            e->tcall_ev.clear();  // no call is open
+            return rc;
+        }
     }
     return GOL_OK;
 }
@@ -1125,6 +1130,7 @@ extern "C" int gol_engine_step_counted(gol_engine *e, int64_t turns, int64_t eve
         for (auto &s : e->sh) s.batch_zero = false;
     }
     if (rc == GOL_OK) rc = timing_end(e);
+    else e->tcall_ev.clear();  // (a failed call is not timed: the timing queries stay usable)
     if (rc != GOL_OK) {
         (void)sync_all(e);
         return rc;
