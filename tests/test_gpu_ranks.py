@@ -264,6 +264,19 @@ def test_bench_share_gpu_weak_board_parity(G):
     assert par["status"] == "ok" and par["turns_checked"] == d["config"]["turns_done"], par
 
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_share_gpu_ring_parity(G, n):
+    """The bench's rank ring at N = 4 and 8 (the driver's SCALE rank counts) on one GPU over IPC:
+    4096 x 65536 split into N shares of 4096 / N rows -- the same torus as the N = 2 and the one-GPU
+    runs -- every count of the run against its one-GPU series."""
+    rc, d, err = _bench(["--gpus", str(n), "--share-gpu", "--rows-per-gpu", str(4096 // n), "--width", "65536",
+                         "--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--settle-s", "0"])
+    assert rc == 0 and d, err
+    par = d["config"]["parity"]
+    assert d["config"]["parallelism"] == f"rows{n}" and par["status"] == "ok" and par["ranks"] == ["ok"] * n, par
+    assert d["config"]["rank_stats"]["nranks_seen"] == [n] * n
+
+
 def test_bench_mispaired_halo_fails_the_line(G):
     """A build whose ranks put each received halo block in the wrong ghost rows
     (libgolhip_mispair.so, GOL_TEST_MISPAIR) computes a plausible but wrong torus: bench.py's
