@@ -928,10 +928,23 @@ band_pipe_kernel(BitsArgs a)
         const char *g0 = st_row;
         st_row += RPB * row_step;
         if ((uint32_t)(b - ib_lo) < ib_n) {
-#pragma unroll
-            for (int s = 0; s < RPB; ++s)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g0 + s * row_step + lane_off), slot + s * ROW, 16,
-                                                 0, GOL_BAND_LOAD_AUX);
+            // The block's two rows as two LDS-DMA loads in the SGPR-base form (the row address in
+            // an SGPR pair, the lane's 32-bit offset in a VGPR): the builtin's address computation
+            // made the compiler use the 64-bit VGPR-address form here, one v_lshl_add_u64 and a
+            // VGPR pair read per load.  Same box, 3 reps: weak +0.6-1.0 %, 262144^2 +-0
+            // (profiles/r06/r06_ab_saddr.jsonl).  M0 (the LDS destination) is written and
+            // restored inside the statement, one wait state before each load (the hazard scan of
+            // tools/check_lds_wait.py checks it); s_nop 4 first covers an SGPR base that a VALU
+            // (readfirstlane) may have written.
+            static_assert(RPB == 2 && GOL_BAND_LOAD_AUX == 0, "two rows per block, default cache policy");
+            uint32_t keep;
+            const char *g1 = g0 + row_step;
+            asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                         "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                         "global_load_lds_dwordx4 %1, %5\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(lane_off), "s"(slot), "s"(g0), "s"(slot + ROW), "s"(g1)
+                         : "memory");
             return;
         }
 #pragma unroll
