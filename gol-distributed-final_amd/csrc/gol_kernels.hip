@@ -1564,16 +1564,36 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
     const int ib_hi = dir >= 0 ? div_floor(in_hi - (RPB - 1) - y_first, RPB) : div_floor(y_first - (RPB - 1) - in_lo, RPB);
     const uint32_t ib_n = ib_hi >= ib_lo ? (uint32_t)(ib_hi - ib_lo + 1) : 0u;
     const char *st_g = mid_b + (int64_t)y_first * pitch + lane_off;
+    const char *st_u = mid_b + (int64_t)y_first * pitch;  // (the same row, wave-uniform)
     constexpr int IROW = 2 * 256;  // uint32 per input row in LDS (two 16-byte halves of 64 lanes)
     auto stage_in = [&](int b, lds_u32 *slot) {
         const char *g = st_g;
         st_g += RPB * row_step;
+        const char *gu = st_u;
+        st_u += RPB * row_step;
         if ((uint32_t)(b - ib_lo) < ib_n) {
-#pragma unroll
-            for (int S = 0; S < RPB; ++S) {
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step), slot + S * IROW, 16, 0, 0);
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + S * row_step + 16), slot + S * IROW + 256, 16, 0, 0);
-            }
+            // The block's 8 LDS-DMA loads in the SGPR-base form, as the band loader's (row address
+            // in an SGPR pair, the lane's 32-bit offset -- and +16 for a row's second half -- in a
+            // VGPR; M0 set and restored inside, a wait state before each load): the builtin made
+            // the compiler compute a 64-bit VGPR address per load.  Same box, 3 reps: 16384^2
+            // bytes 63.0 -> 63.7 TCUPS (profiles/r06/r06_ab_bsaddr.jsonl).
+            static_assert(RPB == 4, "four rows per block");
+            const char *r0 = gu, *r1 = r0 + row_step, *r2 = r1 + row_step, *r3 = r2 + row_step;  // row bases
+            uint32_t keep;
+            asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\t"
+                         "s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %7\n\t"
+                         "s_add_u32 m0, %3, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %7\n\t"
+                         "s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %8\n\t"
+                         "s_add_u32 m0, %4, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %8\n\t"
+                         "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %9\n\t"
+                         "s_add_u32 m0, %5, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %9\n\t"
+                         "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %10\n\t"
+                         "s_add_u32 m0, %6, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %10\n\t"
+                         "s_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(lane_off), "v"(lane_off + 16u), "s"(slot), "s"(slot + IROW), "s"(slot + 2 * IROW),
+                           "s"(slot + 3 * IROW), "s"(r0), "s"(r1), "s"(r2), "s"(r3)
+                         : "memory", "scc");
             return;
         }
 #pragma unroll
