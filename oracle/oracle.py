@@ -192,6 +192,55 @@ def bits_run(words: np.ndarray, turns: int, with_counts: bool = False):
     return (w, counts[:turns]) if with_counts else w
 
 
+# ------------------------------------------ the same restatement, multi-threaded and in place
+# (oracle/gol_oracle_mt.c -> liboracle_mt.so): the count series of full-size boards
+# (tools/pin_counts_oracle.py), cross-checked against bits_run in tests/test_oracle.py.
+_MT_PATH = os.path.join(_HERE, "liboracle_mt.so")
+_mt = None
+
+
+def mt_lib():
+    global _mt
+    if _mt is None:
+        src = os.path.join(_HERE, "gol_oracle_mt.c")
+        if not os.path.exists(_MT_PATH) or os.path.getmtime(_MT_PATH) < os.path.getmtime(src):
+            build()
+        L = ctypes.CDLL(_MT_PATH)
+        L.oracle_mt_bits_run.argtypes = [P, i64, i64, i64, i64, P, ctypes.c_int]
+        L.oracle_mt_bits_run.restype = ctypes.c_int
+        L.oracle_mt_random_words.argtypes = [u64, i64, i64, P, ctypes.c_int]
+        L.oracle_mt_random_words.restype = None
+        L.oracle_mt_hash_words.argtypes = [P, i64, i64, ctypes.c_int]
+        L.oracle_mt_hash_words.restype = u64
+        _mt = L
+    return _mt
+
+
+def mt_random_words(seed: int, H: int, Ww: int, threads: int = 8) -> np.ndarray:
+    """random_words(seed, 0, H, Ww), filled by `threads` threads."""
+    out = np.empty((H, Ww), dtype=np.uint64)
+    mt_lib().oracle_mt_random_words(seed, H, Ww, _ptr(out), threads)
+    return out
+
+
+def mt_hash_words(words: np.ndarray, threads: int = 8) -> int:
+    assert words.dtype == np.uint64 and words.flags.c_contiguous
+    H, Ww = words.shape
+    return int(mt_lib().oracle_mt_hash_words(_ptr(words), H, Ww, threads))
+
+
+def mt_bits_run(words: np.ndarray, turns: int, every: int = 1, threads: int = 8) -> np.ndarray:
+    """`turns` generations IN PLACE on `words` (C-contiguous uint64 rows); returns the alive
+    counts after turns every, 2*every, ... (turns // every of them)."""
+    assert words.dtype == np.uint64 and words.flags.c_contiguous and words.ndim == 2
+    H, Ww = words.shape
+    counts = np.zeros(max(turns // every, 1), dtype=np.int64)
+    rc = mt_lib().oracle_mt_bits_run(_ptr(words), H, Ww, turns, every, _ptr(counts), threads)
+    if rc != 0:
+        raise ValueError("oracle_mt_bits_run failed")
+    return counts[: turns // every]
+
+
 def to_band(words: np.ndarray) -> np.ndarray:
     """Standard bit rows (uint64, 64 cells per word) -> band rows as uint32 words:
     band word w of a row holds at bit b the cell x = b*Wd + w (Wd = W/32).  This is
