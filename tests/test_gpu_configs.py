@@ -204,3 +204,41 @@ def test_config5_full_board_one_gpu(G):
         assert seen["checked"] > 100
     finally:
         _free_engine(e)
+
+
+def _oracle_counts():
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_counts.json")
+    if not os.path.exists(path):
+        return {}
+    import json
+    with open(path) as f:
+        return json.load(f)["boards"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("key", sorted(_oracle_counts()))
+def test_oracle_count_series(G, key):
+    """The bench's random boards (`Engine.load_random(1)`, as bench.py loads them) at their full
+    size, stepped on one GPU to the last turn the CPU oracle computed (tests/golden/oracle_counts.json,
+    tools/pin_counts_oracle.py): every count -- the fused count of each launch -- and the final
+    board's hash equal the oracle's.  Config 2's 16384^2 board runs on the byte board the byte16k
+    line times (`layout="bytes"`, k = 32), the others on the bit board (k = 12)."""
+    rec = _oracle_counts()[key]
+    H, W, every, turns = rec["H"], rec["W"], rec["every"], rec["turns"]
+    assert turns == every * len(rec["counts"]) and rec["hash_final"] is not None
+    layout = "bytes" if key == "16384x16384" else None
+    kw = {"layout": layout} if layout else {}
+    with G.Engine(H, W, device=0, **kw) as e:
+        assert e.info()["turns_per_launch"] == (32 if layout else 12)
+        e.load_random(1)
+        counts = []
+        chunk = every * 500
+        while len(counts) * every < turns:
+            n = min(chunk, turns - len(counts) * every)
+            counts += [int(c) for c in e.step_counted(n, every)]
+        assert counts == rec["counts"]
+        if layout:
+            h = O.hash_words(O.pack(e.store_bytes()))
+        else:
+            h = e.hash()
+    assert h == rec["hash_final"]
