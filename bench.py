@@ -50,6 +50,8 @@ KERNEL_SRCS = [os.path.join(ROOT, "gol-distributed-final_amd", "csrc", f)
 # reference alive-count series of the bench boards (tools/make_bench_counts.py: one GPU, one shard,
 # no exchange); every count of a run is checked against them (`parity` in the line)
 COUNTS_FIXTURE = os.path.join(ROOT, "tests", "golden", "bench_counts.json")
+# the same series from the CPU oracle, over a prefix (tools/pin_counts_oracle.py)
+ORACLE_COUNTS = os.path.join(ROOT, "tests", "golden", "oracle_counts.json")
 # nominal rates of the settle steps (bench.py --settle-s): ~the measured 1-GPU rates
 SETTLE_RATE_BITS = 145e12
 SETTLE_RATE_BYTES = 58e12
@@ -272,11 +274,26 @@ def parity(ranks, board, every, series):
         else:
             mine = {"status": "ok" if n == len(series) else "partial", "points": n, "turns_checked": n * every,
                     "turns_done": len(series) * every}
+    # the run's counts against the CPU oracle's series of the board, over the turns it holds
+    try:
+        with open(ORACLE_COUNTS) as f:
+            orc = json.load(f)["boards"].get(board)
+    except (OSError, ValueError, KeyError):
+        orc = None
+    if orc and orc.get("every") == every:
+        m = min(len(orc["counts"]), len(series))
+        bad = next((i for i in range(m) if series[i] != orc["counts"][i]), None)
+        mine["oracle"] = {"status": "ok" if bad is None else "FAIL", "turns_checked": m * every}
+        if bad is not None:
+            mine["status"] = "FAIL"
+            mine.setdefault("turn", (bad + 1) * every)
     allr = ranks.gather(mine)
     worst = next((r for r in allr if r["status"] == "FAIL"), None) or \
         next((r for r in allr if r["status"] != "ok"), None) or mine
     out = dict(worst)
     out["reference"] = f"tests/golden/bench_counts.json[{board}] (one GPU, one shard, no exchange)"
+    if "oracle" in out:
+        out["oracle"]["reference"] = f"tests/golden/oracle_counts.json[{board}] (CPU oracle)"
     if ranks.world > 1:
         out["ranks"] = [r["status"] for r in allr]
     return out

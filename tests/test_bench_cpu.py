@@ -104,6 +104,15 @@ def test_parity_check_against_reference_series(tmp_path, monkeypatch):
     assert bench.parity(r, "8x64", 4, [10, 11, 12, 13, 14])["status"] == "partial"
     assert bench.parity(r, "8x64", 8, [11])["status"] == "unpinned"
     assert bench.parity(r, "16x64", 4, [1])["status"] == "unpinned"
+    # and against the CPU oracle's series (tests/golden/oracle_counts.json) over the turns it holds
+    orc = tmp_path / "oracle.json"
+    orc.write_text(json.dumps({"boards": {"8x64": {"every": 4, "counts": [10, 11]}}}))
+    monkeypatch.setattr(bench, "ORACLE_COUNTS", str(orc))
+    ok = bench.parity(r, "8x64", 4, [10, 11, 12])
+    assert ok["status"] == "ok" and ok["oracle"]["status"] == "ok" and ok["oracle"]["turns_checked"] == 8
+    orc.write_text(json.dumps({"boards": {"8x64": {"every": 4, "counts": [10, 12]}}}))
+    bad = bench.parity(r, "8x64", 4, [10, 11, 12])
+    assert bad["status"] == "FAIL" and bad["oracle"]["status"] == "FAIL" and bad["turn"] == 8
 
 
 def _fixture():

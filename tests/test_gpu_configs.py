@@ -221,11 +221,11 @@ def test_oracle_count_series(G, key):
     """The bench's random boards (`Engine.load_random(1)`, as bench.py loads them) at their full
     size, stepped on one GPU to the last turn the CPU oracle computed (tests/golden/oracle_counts.json,
     tools/pin_counts_oracle.py): every count -- the fused count of each launch -- and the final
-    board's hash equal the oracle's.  Config 2's 16384^2 board runs on the byte board the byte16k
+    board's hash equal the oracle's (the hash once the oracle's series is complete).  Config 2's 16384^2 board runs on the byte board the byte16k
     line times (`layout="bytes"`, k = 32), the others on the bit board (k = 12)."""
     rec = _oracle_counts()[key]
     H, W, every, turns = rec["H"], rec["W"], rec["every"], rec["turns"]
-    assert turns == every * len(rec["counts"]) and rec["hash_final"] is not None
+    assert turns == every * len(rec["counts"]) and turns > 0
     layout = "bytes" if key == "16384x16384" else None
     kw = {"layout": layout} if layout else {}
     with G.Engine(H, W, device=0, **kw) as e:
@@ -237,6 +237,8 @@ def test_oracle_count_series(G, key):
             n = min(chunk, turns - len(counts) * every)
             counts += [int(c) for c in e.step_counted(n, every)]
         assert counts == rec["counts"]
+        if rec["hash_final"] is None:  # (a series the script has not finished: its counts only)
+            return
         if layout:
             h = O.hash_words(O.pack(e.store_bytes()))
         else:
