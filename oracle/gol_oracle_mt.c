@@ -30,12 +30,12 @@
  * ~1 ms per generation on this container's VM (8 threads no faster than 1 on a 128 MiB board). */
 struct spin_bar {
     int n;
-    int count;      /* arrivals in this phase */
-    int phase;
+    int count;       /* arrivals in this phase */
+    unsigned phase;
 };
 static void bar_wait(struct spin_bar *b)
 {
-    const int ph = __atomic_load_n(&b->phase, __ATOMIC_ACQUIRE);
+    const unsigned ph = __atomic_load_n(&b->phase, __ATOMIC_ACQUIRE);
     if (__atomic_add_fetch(&b->count, 1, __ATOMIC_ACQ_REL) == b->n) {
         __atomic_store_n(&b->count, 0, __ATOMIC_RELAXED);
         __atomic_store_n(&b->phase, ph + 1, __ATOMIC_RELEASE);
@@ -98,6 +98,7 @@ struct mt_ctx {
     int T;
     struct spin_bar bar;
     uint64_t *part;  /* per-thread counts of the current generation */
+    uint64_t *rows;  /* 4 rows of scratch per thread */
 };
 
 struct mt_arg {
@@ -112,7 +113,7 @@ static void *mt_thread(void *p)
     const int64_t H = x->H, Ww = x->Ww, T = x->T, t = g->t;
     const int64_t y0 = H * t / T, y1 = H * (t + 1) / T;
     const size_t rb = (size_t)Ww * sizeof(uint64_t);
-    uint64_t *buf = (uint64_t *)malloc(4 * rb);
+    uint64_t *buf = x->rows + 4 * Ww * t;
     uint64_t *top = buf, *bot = buf + Ww, *prev = buf + 2 * Ww, *cur = buf + 3 * Ww;
     for (int64_t turn = 0; turn < x->turns; turn++) {
         /* the halo rows as they are before this generation (their owners write them after the barrier) */
@@ -138,7 +139,6 @@ static void *mt_thread(void *p)
             x->counts[(turn + 1) / x->every - 1] = (int64_t)c;
         }
     }
-    free(buf);
     return NULL;
 }
 
@@ -152,9 +152,13 @@ int oracle_mt_bits_run(uint64_t *words, int64_t H, int64_t Ww, int64_t turns, in
     x.words = words; x.H = H; x.Ww = Ww; x.turns = turns; x.every = every; x.counts = counts;
     x.T = threads > H ? (int)H : threads;
     x.part = (uint64_t *)calloc((size_t)x.T, sizeof(uint64_t));
+    x.rows = (uint64_t *)malloc((size_t)x.T * 4 * (size_t)Ww * sizeof(uint64_t));
     struct mt_arg *args = (struct mt_arg *)calloc((size_t)x.T, sizeof *args);
     pthread_t *tid = (pthread_t *)calloc((size_t)x.T, sizeof *tid);
-    if (!x.part || !args || !tid) return -2;
+    if (!x.part || !x.rows || !args || !tid) {
+        free(x.part); free(x.rows); free(args); free(tid);
+        return -2;
+    }
     x.bar.n = x.T;
     x.bar.count = 0;
     x.bar.phase = 0;
@@ -164,7 +168,7 @@ int oracle_mt_bits_run(uint64_t *words, int64_t H, int64_t Ww, int64_t turns, in
         pthread_create(&tid[i], NULL, mt_thread, &args[i]);
     }
     for (int i = 0; i < x.T; i++) pthread_join(tid[i], NULL);
-    free(tid); free(args); free(x.part);
+    free(tid); free(args); free(x.part); free(x.rows);
     return 0;
 }
 
@@ -199,9 +203,10 @@ static void *fill_thread(void *p)
 
 static uint64_t fill_or_hash(uint64_t seed, uint64_t *words, int64_t H, int64_t Ww, int threads, int mode)
 {
-    const int T = threads > H ? (int)H : (threads < 1 ? 1 : threads);
-    struct fill_arg *a = (struct fill_arg *)calloc((size_t)T, sizeof *a);
-    pthread_t *tid = (pthread_t *)calloc((size_t)T, sizeof *tid);
+    int T = threads > 64 ? 64 : (threads < 1 ? 1 : threads);
+    if (T > H) T = (int)H;
+    struct fill_arg a[64];
+    pthread_t tid[64];
     for (int i = 0; i < T; i++) {
         a[i].seed = seed; a[i].words = words; a[i].Ww = Ww; a[i].mode = mode;
         a[i].y0 = H * i / T;
@@ -213,7 +218,6 @@ static uint64_t fill_or_hash(uint64_t seed, uint64_t *words, int64_t H, int64_t 
         pthread_join(tid[i], NULL);
         h += a[i].h;
     }
-    free(tid); free(a);
     return h;
 }
 
