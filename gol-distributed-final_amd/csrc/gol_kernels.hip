@@ -1504,6 +1504,10 @@ __device__ __forceinline__ void spstage(PairState<1> &s, uint32_t &r0, uint32_t 
 #ifndef GOL_BYTES_NSI
 #define GOL_BYTES_NSI 3
 #endif
+// Cache policy bits of the byte pipeline's output stores (0: default)
+#ifndef GOL_BYTES_STORE_AUX
+#define GOL_BYTES_STORE_AUX 0
+#endif
 template <int KW, int P, bool COUNT>
 __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 8))) bytes_pipe_kernel(BytesKArgs a)
 {
@@ -1563,12 +1567,9 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
     const int ib_lo = dir >= 0 ? div_ceil_nn(in_lo - y_first, RPB) : div_ceil_nn(y_first - in_hi, RPB);
     const int ib_hi = dir >= 0 ? div_floor(in_hi - (RPB - 1) - y_first, RPB) : div_floor(y_first - (RPB - 1) - in_lo, RPB);
     const uint32_t ib_n = ib_hi >= ib_lo ? (uint32_t)(ib_hi - ib_lo + 1) : 0u;
-    const char *st_g = mid_b + (int64_t)y_first * pitch + lane_off;
-    const char *st_u = mid_b + (int64_t)y_first * pitch;  // (the same row, wave-uniform)
+    const char *st_u = mid_b + (int64_t)y_first * pitch;  // the next block's first row (wave-uniform)
     constexpr int IROW = 2 * 256;  // uint32 per input row in LDS (two 16-byte halves of 64 lanes)
     auto stage_in = [&](int b, lds_u32 *slot) {
-        const char *g = st_g;
-        st_g += RPB * row_step;
         const char *gu = st_u;
         st_u += RPB * row_step;
         if ((uint32_t)(b - ib_lo) < ib_n) {
@@ -1654,8 +1655,8 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
         uint2 e[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) e[q] = lut[(o >> (8 * q)) & 0xFF];
-        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[0].x, e[0].y, e[1].x, e[1].y}, strip_rs, voff, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[2].x, e[2].y, e[3].x, e[3].y}, strip_rs, voff + 16u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[0].x, e[0].y, e[1].x, e[1].y}, strip_rs, voff, 0, GOL_BYTES_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u32{e[2].x, e[2].y, e[3].x, e[3].y}, strip_rs, voff + 16u, 0, GOL_BYTES_STORE_AUX);
         if constexpr (COUNT) {
             const uint32_t c = __popc(o) + alive;
             alive = (uint32_t)rrel < nrows ? c : alive;
