@@ -922,6 +922,9 @@ static int batch_begin(gol_engine *e, int64_t ci)
 #ifndef GOL_LAZY_EVENTS
 #define GOL_LAZY_EVENTS 1
 #endif
+#ifndef GOL_HALO_ON_COMPUTE
+#define GOL_HALO_ON_COMPUTE 1
+#endif
 static int launch_k(gol_engine *e, int k, int64_t count_ci)
 {
     const bool count = count_ci >= 0;
@@ -929,23 +932,27 @@ static int launch_k(gol_engine *e, int k, int64_t count_ci)
     if (!e->halo_ok) RCCHK(exchange_current(e));
     const int n = (int)e->sh.size();
     bool serial = true;  // every shard's launches on its compute stream
+    for (int i = 0; i < n; ++i) serial &= step_mode(e, e->sh[i], k) == GOL_STEP_SERIAL;
+    // the next step's halo: RCCL after a SERIAL step goes on the compute streams themselves
+    const bool on_compute = GOL_HALO_ON_COMPUTE && serial && e->transport == GOL_TRANSPORT_RCCL;
+    // A step whose events no other stream reads records none: one shard with nothing to exchange,
+    // or an RCCL exchange on the compute streams, and every launch on the compute stream.  Each
+    // record is a marker between two band launches that left the GPU idle ~10 us (65536^2: 3 % of
+    // a 0.33 ms launch).  ev_edge then keeps an older record, which later waits pass at once
+    // (they are all on the compute stream).
+    const bool quiet = GOL_LAZY_EVENTS && (local_wrap(e) || on_compute);
     for (int i = 0; i < n; ++i) {
         gol_shard &s = e->sh[i];
         RCCHK(set_dev(s.device));
         gol_launch plan[3];
         int32_t np = 0;
         const int mode = step_mode(e, s, k);
-        serial &= mode == GOL_STEP_SERIAL;
         RCCHK(gol_step_plan(s.R, k, e->kx, mode, plan, 3, &np));
         uint64_t *slots = count ? batch_slots(s, count_ci) : nullptr;  // (zeroed: batch_begin)
         if (timing_open(e)) e->tcall_cells[i] += (double)s.R * (double)e->W * k;
-        // One shard with nothing to exchange, every launch on the compute stream: the step's two
-        // events would be read by no other stream, and each record is a marker between two band
-        // launches that left the GPU idle ~10 us (65536^2: 3 % of a 0.33 ms launch).  Skip them
-        // (ev_edge keeps an older record, which later waits pass at once).
         bool plan_edge = false;
         for (int j = 0; j < np; ++j) plan_edge |= plan[j].stream == GOL_LAUNCH_EDGE;
-        const bool markers = !(GOL_LAZY_EVENTS && local_wrap(e) && !plan_edge);
+        const bool markers = !(quiet && !plan_edge);
         if (markers) HIPCHK(hipEventRecord(s.ev_start, s.stream));  // the step's inputs are complete, slots zeroed
         bool edge_used = false, waited[2] = {false, false};
         int last_halo = -1;  // the last launch that reads the halo writes the rows the exchange sends
@@ -972,11 +979,8 @@ static int launch_k(gol_engine *e, int k, int64_t count_ci)
     }
     if (timing_open(e)) e->tcall_steps += 1;
     e->cur = 1 - e->cur;
-    // the next step's halo: waits only for each shard's ev_edge
-#ifndef GOL_HALO_ON_COMPUTE
-#define GOL_HALO_ON_COMPUTE 1
-#endif
-    e->halo_on_compute = GOL_HALO_ON_COMPUTE && serial && e->transport == GOL_TRANSPORT_RCCL;
+    // the next step's halo: waits only for each shard's ev_edge (or, on_compute, stream order)
+    e->halo_on_compute = on_compute;
     RCCHK(exchange(e, e->halo_on_compute));
     e->halo_ok = true;
     return GOL_OK;
