@@ -2600,10 +2600,17 @@ static bool rank_split(int64_t rows, int64_t ngroups, int cus, int per_cu, const
 static const double BAND_PIPE_RANK_W[4] = {GOL_BAND_RANK_W};
 static const double BYTES_PIPE_RANK_W[4] = {GOL_BYTES_RANK_W};
 
-// Rounds of half-length tail strips (StripMap.tail_*): same box, 2^17 x 2^20: none 137.2 TCUPS,
-// 0.5 round 138.8, 1.0 138.8, 1.5 138.6; 262144^2: 132.2 / 133.6 / 133.2 / 133.0.
+// Rounds of short tail strips (StripMap.tail_*), 1 / GOL_BAND_TAIL_DIV of a strip's rows each.
+// Round 3, half-length strips, same box, 2^17 x 2^20: none 137.2 TCUPS, 0.5 round 138.8, 1.0
+// 138.8, 1.5 138.6; 262144^2: 132.2 / 133.6 / 133.2 / 133.0.  Round 6, weak board, two boxes, 3 + 4
+// reps against half-length strips for 0.5 round: quarter-length strips for 1 round +0.5 / +0.6 %,
+// for 0.5 round +0.1 %, 0.25 round -1.1 %, 1.5 rounds -0.4 %; third-length -0.3 %, eighth-length
+// -0.1 % (profiles/r06/r06_ab_tail.log).
 #ifndef GOL_BAND_TAIL
-#define GOL_BAND_TAIL 0.5
+#define GOL_BAND_TAIL 1.0
+#endif
+#ifndef GOL_BAND_TAIL_DIV
+#define GOL_BAND_TAIL_DIV 4
 #endif
 #ifndef GOL_BAND_PAIRED
 #define GOL_BAND_PAIRED 1
@@ -2667,8 +2674,8 @@ static hipError_t launch_band_pipe(bool contig, BitsArgs a, hipStream_t s, bool 
         if (auto_strip) a.strip = (int)round_tiled_strip(a.rows, a.ngroups, slots, 8 * KW * P, 1024, a.strip);
         nwg = (int64_t)a.ngroups * ((a.rows + a.strip - 1) / a.strip);
         if (auto_strip && GOL_BAND_TAIL > 0 && slots > 0 && nwg > 4 * slots) {
-            // the last ~GOL_BAND_TAIL rounds of workgroups run strips of half the rows
-            const int64_t ts = std::max<int64_t>(8 * KW * P, a.strip / 2);
+            // the last ~GOL_BAND_TAIL rounds of workgroups run strips of 1 / GOL_BAND_TAIL_DIV of the rows
+            const int64_t ts = std::max<int64_t>(8 * KW * P, a.strip / GOL_BAND_TAIL_DIV);
             const int64_t nt = (int64_t)(GOL_BAND_TAIL * (double)slots / a.ngroups + 0.999);  // tail strips per group
             const int64_t tail_rows = std::min<int64_t>(a.rows / 2, nt * ts);
             const int64_t big = a.rows - tail_rows;
