@@ -81,8 +81,9 @@ def test_oracle_series_reproducible(oracle_counts):
 
 def test_bench_series_pinned_to_oracle(oracle_counts):
     """Every point of the GPU series (bench_counts.json) that the oracle holds is the oracle's; the
-    oracle covers BASELINE config 2 (16384^2) and config 3 (65536^2) past their 10,000 turns and the
-    bench's N = 1 weak board past the driver's default run (78 counts, 936 turns)."""
+    oracle covers BASELINE config 2 (16384^2) and config 3 (65536^2) past their 10,000 turns, and the
+    bench's weak board at N = 1 and 2 and the 262144^2 board past the driver's run (78 counts, 936
+    turns)."""
     bench = _load("bench_counts.json")["boards"]
     covered = {}
     for key, rec in oracle_counts["boards"].items():
@@ -96,4 +97,6 @@ def test_bench_series_pinned_to_oracle(oracle_counts):
     assert covered.get("16384x16384", 0) >= 10000
     assert covered.get("65536x65536", 0) >= 10000
     assert covered.get("131072x1048576", 0) >= 936
+    assert covered.get("262144x1048576", 0) >= 936  # the weak board at N = 2 (the driver's SCALE run)
+    assert covered.get("262144x262144", 0) >= 936
     assert covered.get("4096x65536", 0) >= 600
