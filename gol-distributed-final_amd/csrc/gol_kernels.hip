@@ -1579,7 +1579,16 @@ __global__ void __launch_bounds__(64 * P) __attribute__((amdgpu_waves_per_eu(6, 
             // the compiler compute a 64-bit VGPR address per load.  Same box, 3 reps: 16384^2
             // bytes 63.0 -> 63.7 TCUPS (profiles/r06/r06_ab_bsaddr.jsonl).
             static_assert(RPB == 4, "four rows per block");
-            const char *r0 = gu, *r1 = r0 + row_step, *r2 = r1 + row_step, *r3 = r2 + row_step;  // row bases
+            // row bases, wave-uniform: readfirstlane makes that explicit for builds whose control
+            // flow hides it (GOL_SPIN_LIMIT=0: the "s" operands below would get VGPRs); it folds
+            // away where the compiler already keeps them in SGPRs
+            auto uni = [](const char *q) {
+                const uint64_t v = reinterpret_cast<uint64_t>(q);
+                const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+                const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+                return reinterpret_cast<const char *>(lo | (hi << 32));
+            };
+            const char *r0 = uni(gu), *r1 = uni(r0 + row_step), *r2 = uni(r1 + row_step), *r3 = uni(r2 + row_step);
             uint32_t keep;
             asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\t"
                          "s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %7\n\t"
