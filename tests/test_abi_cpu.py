@@ -182,6 +182,27 @@ def test_pipe_kernels_wait_before_reading_lds(tmp_path):
     assert "0 hazards" in r.stdout
 
 
+@pytest.mark.parametrize("unit,flags", [("gol_band_pipe.hip", "BANDFLAGS"), ("gol_bytes_pipe.hip", "BYTEFLAGS")])
+def test_pipe_units_compile_with_test_defines(tmp_path, unit, flags):
+    """The pipeline units under the test builds' defines (`make spintest`: GOL_SPIN_LIMIT=0;
+    `make mispair` changes host code only): their inline asm takes wave-uniform ("s") operands,
+    which another control flow can leave in VGPRs -- the spin-limit build of the byte loader's
+    SGPR-base loads once failed to assemble while the product built."""
+    import re
+    import shutil
+    if shutil.which("/opt/rocm/bin/hipcc") is None:
+        pytest.skip("hipcc not present")
+    csrc = os.path.join(ROOT, "gol-distributed-final_amd", "csrc")
+    mk = open(os.path.join(csrc, "Makefile")).read()
+    sched = re.search(r"^%s = (.*)$" % flags, mk, re.M).group(1).split()
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                        "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"] + sched +
+                       ["-DGOL_SPIN_LIMIT=0", "-I" + os.path.join(ROOT, "include"), "-I" + csrc,
+                        "--cuda-device-only", "-c", os.path.join(csrc, unit), "-o", str(tmp_path / "u.o")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
 def test_valu_hazard_checker_catches_asm_hazards():
     """tools/check_lds_wait.py's VALU-hazard scan (round 6) on hand-made assembly: a v_dot4 result
     read at once, a DPP move of a register an asm VALU just wrote, an asm LDS DMA right after an
